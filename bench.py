@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the final() path-tracing workload on MI355X.
+
+Workload (BASELINE.json configs[3], the metric's config): final() (main.cpp:190-230),
+camera main.cpp:254-259, 1000 spp, depth 50, black background, 500x500 pixels per
+GPU.  One step = one full render of the job: every pixel x every sample, camera
+ray -> path -> BVH/primitive/medium hits -> scatter, through the C ABI's
+persistent HIP megakernel, plus (N > 1) the RCCL gather of the packed tiles to
+rank 0.  Scene upload and BVH build happen before the timed region (inputs
+resident in HBM); the PPM write is not part of a step.
+
+Multi-GPU (torchrun, one process per GPU): weak scaling — N ranks render an image
+of N x 250,000 pixels (500x500, 1000x500, 1000x1000 = config 5's image, 2000x1000),
+interleaved 32x32 tiles (tile k -> rank k % N), then one torch.distributed gather
+(backend "nccl" = RCCL over xGMI) of the packed float tiles to rank 0.
+
+Prints ONE JSON line (rank 0) with roofline (algorithmic bytes / kernel time vs
+8 TB/s HBM) and cpu_baseline (the reference binary on host cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "peter-shirley-ray-tracing-the-next-week_amd")
+ORACLE = os.path.join(ROOT, "oracle")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import rtnw  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+TILE = 32
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def image_for(n):
+    # N x 250k pixels: 500x500, 1000x500, 1000x1000, 2000x1000, ...
+    w, h = 500, 500
+    k = 1
+    while k < n:
+        if w <= h:
+            w *= 2
+        else:
+            h *= 2
+        k *= 2
+    if k != n:   # non power of two: stretch the width
+        w, h = 500 * n, 500
+    return w, h
+
+
+def cpu_baseline(budget_procs):
+    """Reference renderer (oracle/_ref/ref_render, compiled from the reference's own
+    sources) on host cores: final() 500x500 at 2 spp, rows split over P processes."""
+    ref = os.path.join(ORACLE, "_ref", "ref_render")
+    nx, ny, ns = 500, 500, 2
+    P = budget_procs
+    if os.path.exists(ref) and os.access(ref, os.X_OK):
+        bands = [(ny * i // P, ny * (i + 1) // P) for i in range(P)]
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen([ref, "--scene", "final", "--nx", str(nx), "--ny", str(ny), "--ns", str(ns),
+                                   "--rows", f"{a}:{b}"], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                  cwd="/tmp") for a, b in bands]
+        rc = [p.wait() for p in procs]
+        dt = time.perf_counter() - t0
+        if all(r == 0 for r in rc):
+            return {"value": nx * ny * ns / dt / 1e6, "unit": "Msamples/s", "cores": P, "kind": "reference",
+                    "sample": f"final() {nx}x{ny}x{ns}spp, flat list as shipped (main.cpp:291), rows split over "
+                              f"{P} processes of oracle/_ref/ref_render (clang++ -O2), wall {dt:.2f}s"}
+    sys.path.insert(0, ORACLE)
+    import oracle as O
+    spec = O.kernel_spec("final", nx, ny, ns, seed=0, threads=P)
+    _, st = O.render(spec)
+    return {"value": st["samples"] / st["seconds"] / 1e6, "unit": "Msamples/s", "cores": P, "kind": "port",
+            "sample": f"final() {nx}x{ny}x{ns}spp, oracle/rt_oracle.c flat list, OpenMP {P} threads, "
+                      f"{st['seconds']:.2f}s"}
+
+
+def read_traffic(workload):
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == workload:
+            return t.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=1000)
+    ap.add_argument("--chunk", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ppm", default="")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    nx, ny = image_for(world)
+    spp = args.spp
+    tiles = rtnw.tiles_for_rank(nx, ny, TILE, rank, world) if world > 1 else [(0, 0, nx, ny)]
+    all_counts = [sum(w * h for _, _, w, h in rtnw.tiles_for_rank(nx, ny, TILE, r, world)) * 3 for r in range(world)] \
+        if world > 1 else [nx * ny * 3]
+    n_local = all_counts[rank]
+    n_max = max(all_counts)
+
+    scene = rtnw.Scene.builtin("final", device=local)
+    cam = rtnw.Camera.preset("cornell", nx, ny)
+    params = rtnw.RenderParams(nx, ny, spp, max_depth=50, chunk=args.chunk, seed=2024)
+    out = torch.zeros(n_max, dtype=torch.float32, device=dev)
+    gather_list = [torch.empty(n_max, dtype=torch.float32, device=dev) for _ in range(world)] \
+        if (world > 1 and rank == 0) else None
+
+    def step():
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        st = scene.render_tiles(cam, params, tiles, out.data_ptr(), stream, stats=True)
+        if world > 1:
+            dist.gather(out, gather_list, dst=0)
+        return st
+
+    workload = f"c4: final() {nx}x{ny} pixels x {spp} spp, depth 50" + (f" over {world} GPUs" if world > 1 else "")
+    for i in range(args.warmup):
+        st = step()
+        log(f"[rank {rank}] warmup {i}: kernel {st['kernel_ms']:.1f} ms")
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    kms = []
+    for i in range(args.steps):
+        st = step()
+        kms.append(st["kernel_ms"])
+        log(f"[rank {rank}] step {i}: kernel {st['kernel_ms']:.1f} ms")
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_per_step = nx * ny * spp
+    value = samples_per_step * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # roofline of the megakernel: algorithmic bytes (counting launch, same RNG -> same
+    # paths) over the average HIP-event duration of the timed launches on this rank
+    cnt = rtnw.RenderParams(nx, ny, spp, max_depth=50, chunk=args.chunk, seed=2024, flags=rtnw.RT_FLAG_COUNT)
+    cst = scene.render_tiles(cam, cnt, tiles, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream, stats=True)
+    avg_kernel_s = float(np.mean(kms)) / 1e3
+    alg = cst["algorithmic_bytes"]
+    achieved = alg / avg_kernel_s / 1e9
+
+    if rank == 0 and args.ppm and world == 1:
+        img = out[: nx * ny * 3].cpu().numpy().reshape(ny, nx, 3)
+        with open(args.ppm, "wb") as f:
+            f.write(rtnw.ppm_text(rtnw.quantize(img)))
+
+    if rank == 0:
+        res = {
+            "metric": "Msamples/s (pixels×spp/s) + achieved HBM GB/s, final() 500×500×1000spp",
+            "value": value,
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: procedural final() scene (main.cpp:190-230), counter-RNG samples, seed 2024",
+            "config": {"workload": workload, "image": [nx, ny], "spp": spp, "pixels_per_gpu": nx * ny // world,
+                       "tile": TILE if world > 1 else None, "chunk": args.chunk,
+                       "parallelism": f"pixel tiles x{world}" + (" + RCCL gather" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(workload),
+                         "kernel_ms_avg": avg_kernel_s * 1e3,
+                         "algorithmic_bytes_per_launch": alg,
+                         "rays_per_sample": cst["segments"] / max(1.0, cst["samples"]),
+                         "node_visits_per_ray": cst["node_visits"] / max(1.0, cst["segments"]),
+                         "prim_tests_per_ray": cst["prim_tests"] / max(1.0, cst["segments"])},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(min(16, os.cpu_count() or 1))
+        print(json.dumps(res), flush=True)
+    scene.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

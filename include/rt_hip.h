@@ -1,0 +1,211 @@
+/* include/rt_hip.h — C ABI of librt_hip.so, the MI355X path tracer.
+ *
+ * Boundary being replaced (the reference has no FFI; its hot path is a C++ call
+ * pair):
+ *   vec3 color(const ray&, hitable *world, int depth)      main.cpp:25-46
+ *   the per-pixel sample loop of main()                     main.cpp:299-332
+ *   hitable::hit / material::scatter / texture::value       hitable.h:34, material.h:54, texture.h:13
+ * The host keeps the reference's hitable/material/texture/camera classes (see
+ * peter-shirley-ray-tracing-the-next-week_amd/csrc/host/rtnw.h); a world built
+ * with them is flattened into an rt_scene_desc, uploaded once with
+ * rt_scene_create, and rendered on the GPU with rt_render_tile / rt_render_tiles.
+ *
+ * Conventions: plain C types only; every function returns RT_OK (0) or a
+ * negative rt_status; rt_last_error() returns a thread-local message.  A scene is
+ * bound to one HIP device; calls on one scene are serialised on a stream.  There
+ * is no CPU fallback: without a usable GPU every render entry point fails.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,      /* bad argument / malformed descriptor */
+    RT_ERR_HIP = -2,          /* HIP runtime failure (no device, launch error, ...) */
+    RT_ERR_NOMEM = -3,
+    RT_ERR_UNSUPPORTED = -4   /* a scene feature the device path does not implement */
+} rt_status;
+
+/* ------------------------------------------------------------ scene descriptor
+ * Flattened form of a hitable tree.  Leaves are listed in depth-first list order
+ * (the order hitable_list::hit visits them, hitable_list.h:24); that order is the
+ * tie-break order of the closest-hit search.                                   */
+enum rt_prim_kind {
+    RT_PRIM_SPHERE = 0,          /* sphere.h:10-52:  p = {cx, cy, cz, r}                      */
+    RT_PRIM_MOVING_SPHERE = 1,   /* sphere.h:61-118: p = {c0x,c0y,c0z, c1x,c1y,c1z, t0, t1, r} */
+    RT_PRIM_XY_RECT = 2,         /* aarect.h:11-65:  p = {x0, x1, y0, y1, k}                  */
+    RT_PRIM_XZ_RECT = 3,         /* aarect.h:23-83:  p = {x0, x1, z0, z1, k}                  */
+    RT_PRIM_YZ_RECT = 4          /* aarect.h:35-100: p = {y0, y1, z0, z1, k}                  */
+};
+
+typedef struct rt_prim {
+    int32_t kind;        /* rt_prim_kind */
+    int32_t material;    /* index into rt_scene_desc.materials */
+    int32_t instance;    /* -1, or index into rt_scene_desc.instances (transform chain) */
+    int32_t flip;        /* 1: a flip_normals wraps the primitive directly (hitable.h:39-54) */
+    float p[12];
+} rt_prim;               /* 64 bytes */
+
+enum rt_xform_op {
+    RT_OP_TRANSLATE = 1, /* hitable.h:57-83:  {ox, oy, oz}            */
+    RT_OP_ROTATE_Y = 2,  /* hitable.h:85-150: {sin_theta, cos_theta}  */
+    RT_OP_FLIP = 3       /* hitable.h:39-54 between two transforms    */
+};
+
+typedef struct rt_instance {
+    int32_t nops;        /* <= 6; ops[0] is the outermost wrapper */
+    int32_t pad[3];
+    float ops[6][4];     /* {op, a, b, c} */
+} rt_instance;
+
+enum rt_material_kind {
+    RT_MAT_LAMBERTIAN = 0,    /* material.h:61-72   texture        */
+    RT_MAT_METAL = 1,         /* material.h:74-85   albedo, fuzz   */
+    RT_MAT_DIELECTRIC = 2,    /* material.h:87-123  ref_idx        */
+    RT_MAT_DIFFUSE_LIGHT = 3, /* material.h:126-139 texture        */
+    RT_MAT_ISOTROPIC = 4      /* material.h:142-151 texture        */
+};
+
+typedef struct rt_material {
+    int32_t kind;
+    int32_t texture;     /* -1 when unused */
+    float fuzz;          /* already clamped to <= 1 (material.h:76) */
+    float ref_idx;
+    float albedo[3];
+    int32_t pad;
+} rt_material;           /* 32 bytes */
+
+enum rt_texture_kind {
+    RT_TEX_CONSTANT = 0, /* texture.h:16-27 color                    */
+    RT_TEX_CHECKER = 1,  /* texture.h:30-45 even, odd (texture idx)  */
+    RT_TEX_NOISE = 2,    /* texture.h:48-59 scale                    */
+    RT_TEX_IMAGE = 3     /* surface_texture.h:10-30 (not yet on device) */
+};
+
+typedef struct rt_texture {
+    int32_t kind;
+    int32_t even, odd;
+    float scale;
+    float color[3];
+    int32_t image;
+} rt_texture;            /* 32 bytes */
+
+typedef struct rt_medium {   /* constant_medium.h:14-50 */
+    int32_t boundary_first;  /* range in rt_scene_desc.boundary_prims */
+    int32_t boundary_count;
+    float density;
+    int32_t material;        /* the isotropic phase material */
+    int32_t order;           /* number of surface prims before it in list order */
+    int32_t pad[3];
+} rt_medium;
+
+typedef struct rt_scene_desc {
+    uint32_t abi_version;         /* RT_ABI_VERSION */
+    int32_t nprims, nboundary, nmedia, nmaterials, ntextures, ninstances;
+    const rt_prim *prims;         /* surfaces, depth-first list order */
+    const rt_prim *boundary_prims;/* leaves of media boundaries */
+    const rt_medium *media;       /* in list order (= keyed-draw ordinal) */
+    const rt_material *materials;
+    const rt_texture *textures;
+    const rt_instance *instances;
+    const float *perlin_ranvec;   /* 256 x 3, perlin.h:82-87 */
+    const int32_t *perlin_perm;   /* 3 x 256, perlin.h:99-111 */
+    float time0, time1;           /* shutter span rays may carry (moving-sphere bounds) */
+} rt_scene_desc;
+
+/* ------------------------------------------------------------------ camera */
+typedef struct rt_camera_desc {   /* the state camera.h:21-39 computes */
+    float origin[3], lower_left_corner[3], horizontal[3], vertical[3], u[3], v[3], w[3];
+    float lens_radius, time0, time1;
+} rt_camera_desc;
+
+/* Same arithmetic as camera::camera (camera.h:21-39). */
+int rt_camera_init(rt_camera_desc *out, const float lookfrom[3], const float lookat[3], const float vup[3],
+                   float vfov, float aspect, float aperture, float focus_dist, float t0, float t1);
+
+/* ------------------------------------------------------------------ render */
+enum { RT_BG_BLACK = 0, RT_BG_SKY = 1 };
+enum { RT_FLAG_COUNT = 1 };       /* run the counting variant: fills the rt_stats visit counters */
+
+typedef struct rt_render_params {
+    int32_t nx, ny;               /* full image (u,v normalisation and pixel keys) */
+    int32_t spp;                  /* samples per pixel (main.cpp:251 ns) */
+    int32_t max_depth;            /* scatter while depth < max_depth (main.cpp:34: 50) */
+    float t_min;                  /* main.cpp:27: 0.001 */
+    int32_t background;           /* RT_BG_* */
+    int32_t chunk;                /* samples per partial sum; <= 0 selects 16 */
+    int32_t flags;                /* RT_FLAG_* */
+    uint32_t sample_offset;       /* first sample index (progressive rendering) */
+    uint32_t pad;
+    uint64_t seed;                /* counter-RNG key */
+} rt_render_params;
+
+typedef struct rt_stats {
+    double samples;               /* camera samples rendered */
+    double segments;              /* rays traced (RT_FLAG_COUNT) */
+    double node_visits;           /* BVH nodes fetched (RT_FLAG_COUNT) */
+    double prim_tests;            /* primitive intersection tests (RT_FLAG_COUNT) */
+    double medium_tests;          /* constant_medium evaluations (RT_FLAG_COUNT) */
+    double noise_evals;           /* Perlin turbulence evaluations (RT_FLAG_COUNT) */
+    double algorithmic_bytes;     /* SURVEY §8d byte model for the launch (RT_FLAG_COUNT) */
+    double kernel_ms;             /* megakernel time from HIP events on the render stream */
+    double resolve_ms;            /* partial-sum resolve kernel time */
+} rt_stats;
+
+typedef struct rt_scene rt_scene; /* opaque; owns device copies */
+
+/* Copies the descriptor into device memory (HBM) of `device` and builds the BVH.
+ * The caller keeps ownership of d. */
+int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out);
+void rt_scene_destroy(rt_scene *s);
+
+/* Renders the w x h rectangle at (x0, y0) (image coords, row 0 = top row of the
+ * PPM, i.e. main.cpp's j = ny-1) into out_rgb (host memory, h*w*3 floats, linear
+ * mean radiance = main.cpp's `col` after `col /= float(ns)`).  Synchronous. */
+int rt_render_tile(rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p,
+                   int x0, int y0, int w, int h, float *out_rgb, rt_stats *stats);
+
+/* Renders ntiles rectangles (tiles[4k..4k+3] = x0, y0, w, h) into device memory:
+ * out_dev receives the tiles packed back to back (tile k at offset sum_{i<k} w_i*h_i*3
+ * floats, each row-major).  Enqueued on `stream` (a hipStream_t; NULL = default
+ * stream).  When stats is non-NULL the call waits for completion to read the
+ * HIP-event timings. */
+int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p,
+                    const int32_t *tiles, int ntiles, float *out_dev, void *stream, rt_stats *stats);
+
+/* Device buffer helpers, so callers without a HIP toolchain can drive the ABI. */
+int rt_device_alloc(int device, uint64_t bytes, void **out);
+int rt_device_free(void *ptr);
+int rt_copy_to_host(void *dst, const void *src_dev, uint64_t bytes);
+int rt_device_count(int *out);
+
+/* ----------------------------------------------------- resolve (main.cpp:314-330) */
+/* sqrt gamma + int(255.99*c) + clamp to 255, per channel (main.cpp:316-325). */
+void rt_quantize(const float *mean_rgb, int64_t n_pixels, uint8_t *rgb);
+/* P3 text of main.cpp:297,327-330; returns the byte count (writes when buf != NULL and cap suffices). */
+int64_t rt_ppm_text(const uint8_t *rgb, int nx, int ny, char *buf, int64_t cap);
+
+/* ------------------------------------------------ host scene construction */
+/* Builds one of the reference's scenes with the host API (random_scene, random_motion,
+ * cornell_box, cornell_smoke, final, simple_light, two_spheres, test) exactly as a
+ * fresh reference process would (drand48 state 0, Perlin static init first) and
+ * returns its flattened descriptor (free with rt_scene_desc_free). */
+int rt_builtin_scene_desc(const char *name, rt_scene_desc **out);
+void rt_scene_desc_free(rt_scene_desc *d);
+/* Leaf dump in the text format of oracle/ref_harness.cpp --dump (for parity tests). */
+int64_t rt_scene_desc_dump(const rt_scene_desc *d, char *buf, int64_t cap);
+
+const char *rt_last_error(void);
+const char *rt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,45 @@
+// rt_kernel.h — launch interface between the host runtime (capi.cpp) and the
+// megakernel (rt_kernel.hip).  Internal to librt_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RT_BLOCK 256   // 4 waves per workgroup
+
+struct RtKernelArgs {
+    // scene (HBM, 16-B records; see rt_layout.h)
+    const float4 *nodes;    // 4 x float4 per BVH node
+    const float4 *prims;    // 4 x float4 per surface primitive (leaf order)
+    const float4 *bprims;   // 4 x float4 per media-boundary primitive
+    const int4 *media;      // 1 x int4 per medium
+    const float4 *mats;     // 2 x float4 per material
+    const float4 *texs;     // 2 x float4 per texture
+    const float4 *insts;    // 7 x float4 per instance chain
+    const float4 *ranvec;   // 256 Perlin gradients (w unused)
+    const int *perm;        // 3 x 256 Perlin permutations
+    uint32_t root;
+    int has_bvh;
+    int nmedia;
+    // camera (camera.h members)
+    float org[3], llc[3], hor[3], ver[3], cu[3], cv[3];
+    float lens, ct0, ct1;
+    // render parameters
+    int nx, ny, ns, max_depth;
+    float tmin;
+    int background;
+    int chunk, nchunks;
+    uint32_t sample_offset;
+    uint64_t seed;
+    // job: pixel list and outputs
+    const uint32_t *job_xy;   // x | y << 16 per job pixel (image coords)
+    uint32_t npix;
+    uint32_t nitems;          // npix * nchunks
+    float4 *slab;             // [nchunks][npix] partial sums
+    uint32_t *counter;        // work-claim counter (zeroed per launch)
+    unsigned long long *stats;  // RT_CNT_N counters (count variant)
+};
+
+extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, bool count, hipStream_t stream);
+extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k,
+                                        const uint32_t *out_index, float *out, hipStream_t stream);
+extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, bool count);

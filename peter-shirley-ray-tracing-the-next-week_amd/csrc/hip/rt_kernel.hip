@@ -1,0 +1,642 @@
+// rt_kernel.hip — persistent path-tracing megakernel for gfx950 (MI355X).
+//
+// Device restatement of the reference's hot path:
+//   sample loop        main.cpp:299-313   (jitter, get_ray, color, de_nan, col += temp)
+//   camera::get_ray    camera.h:41-56
+//   color()            main.cpp:25-46     (iterative: throughput * emitted)
+//   closest hit        hitable_list.h:20-32 via a BVH2 with exact list-order tie-breaking
+//   sphere / moving_sphere / xy|xz|yz_rect / box / flip_normals / translate / rotate_y
+//   constant_medium    constant_medium.h:26-50 (evaluated after the surface search)
+//   material::scatter  material.h:16-151 ; texture::value texture.h:16-59 ; perlin.h:25-74
+//
+// Execution model (wave64, CDNA4):
+//   * persistent workgroups of 4 waves; each LANE owns one camera path at a time and
+//     regenerates a new camera sample as soon as its path terminates, so lanes stay
+//     busy across bounces (path regeneration) instead of idling until the longest
+//     path of the wave finishes;
+//   * work = (chunk of `chunk` samples) x (pixel); a wave claims 64 work items per
+//     atomic (one global atomic per claim, amortised over 64 chunks) and hands them
+//     to the lanes that need work with a ballot + mbcnt prefix count;
+//   * each item's radiance is summed in registers and stored once into a partial-sum
+//     slab [chunk][pixel]; rt_resolve sums the chunks in order (deterministic, no
+//     float atomics, independent of the number of GPUs);
+//   * the BVH traversal stack lives in LDS, laid out [wave][depth][lane] so every
+//     push/pop of a wave is one conflict-free ds_write_b32/ds_read_b32;
+//   * nodes, primitives and materials are 16-B records read with dwordx4 loads.
+//
+// Arithmetic follows the reference's float/double promotions; the file is compiled
+// with -ffp-contract=off so no FMA is introduced where the reference has none (the
+// BVH slab test, which decides nothing about the result, uses explicit fmaf).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../rt_layout.h"
+#include "rt_kernel.h"
+
+#define RT_FLT_MAX 0x1.fffffep+127f
+#define RT_INF __builtin_huge_valf()
+
+namespace {
+
+// ------------------------------------------------------------------ vec3
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 mk(float a, float b, float c) { V3 r; r.x = a; r.y = b; r.z = c; return r; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 scale(float t, V3 v) { return mk(t * v.x, t * v.y, t * v.z); }
+__device__ __forceinline__ V3 divs(V3 v, float t) { return mk(v.x / t, v.y / t, v.z / t); }
+__device__ __forceinline__ V3 neg(V3 v) { return mk(-v.x, -v.y, -v.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float len(V3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+__device__ __forceinline__ V3 unit(V3 v) { return divs(v, len(v)); }
+__device__ __forceinline__ float comp(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+struct Ray { V3 o, d; float time; };
+__device__ __forceinline__ V3 at(const Ray &r, float t) { return add(r.o, scale(t, r.d)); }
+
+// ------------------------------------------------------------------- RNG
+// Counter streams: sample (pixel, s) draws u48(mix64(key + n*GAMMA)),
+// n = 1, 2, ...; constant_medium k at bounce b draws from a second keyed stream.
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double u48(uint64_t z) { return (double)(z >> 16) * 0x1p-48; }
+__device__ __forceinline__ uint64_t sample_key(uint64_t seed, uint32_t pixel, uint32_t sample) {
+    return mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) ^ (((uint64_t)pixel << 32) | sample));
+}
+struct Rng {
+    uint64_t key;
+    uint32_t n;
+    __device__ __forceinline__ double next() { ++n; return u48(mix64(key + (uint64_t)n * kGamma)); }
+    __device__ __forceinline__ double medium(int bounce, int k) const {
+        uint64_t mkey = mix64(key ^ 0xD1B54A32D192ED03ull);
+        uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
+        return u48(mix64(mkey + (m + 1) * kGamma));
+    }
+};
+
+// ----------------------------------------------------------- scene access
+__device__ __forceinline__ float4 ld4(const float4 *p, uint32_t i) { return p[i]; }
+__device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
+
+// Ray into the object space of an instance chain (hitable.h:66-67, 129-135).
+__device__ __forceinline__ Ray to_object(const float4 *insts, int inst, Ray r) {
+    const float4 *I = insts + inst * 7;
+    int nops = fbits(I[0].x);
+    for (int k = 0; k < nops; ++k) {
+        float4 op = I[1 + k];
+        int code = fbits(op.x);
+        if (code == RT_OP_TRANSLATE) {
+            r.o = sub(r.o, mk(op.y, op.z, op.w));
+        } else if (code == RT_OP_ROTATE_Y) {
+            float s = op.y, c = op.z;
+            V3 o = r.o, d = r.d;
+            o.x = c * r.o.x - s * r.o.z;
+            o.z = s * r.o.x + c * r.o.z;
+            d.x = c * r.d.x - s * r.d.z;
+            d.z = s * r.d.x + c * r.d.z;
+            r.o = o; r.d = d;
+        }
+    }
+    return r;
+}
+
+// Hit point / normal back to world space, innermost wrapper first (hitable.h:43-45, 69, 137-145).
+__device__ __forceinline__ void to_world(const float4 *insts, int inst, V3 &p, V3 &n) {
+    const float4 *I = insts + inst * 7;
+    int nops = fbits(I[0].x);
+    for (int k = nops - 1; k >= 0; --k) {
+        float4 op = I[1 + k];
+        int code = fbits(op.x);
+        if (code == RT_OP_TRANSLATE) {
+            p = add(p, mk(op.y, op.z, op.w));
+        } else if (code == RT_OP_ROTATE_Y) {
+            float s = op.y, c = op.z;
+            V3 q = p, m = n;
+            q.x = c * p.x + s * p.z;
+            q.z = -s * p.x + c * p.z;
+            m.x = c * n.x + s * n.z;
+            m.z = -s * n.x + c * n.z;
+            p = q; n = m;
+        } else if (code == RT_OP_FLIP) {
+            n = neg(n);
+        }
+    }
+}
+
+// Candidate hit distance of one primitive for a search starting at t_min with no
+// upper bound (RT_INF = miss).  The caller keeps the closest (t, key) pair, which
+// reproduces hitable_list's sequential `t < closest` / `t <= closest` acceptance.
+__device__ __forceinline__ float sphere_t(V3 c, float rad, const Ray &r, float tmin) {   // sphere.h:25-52
+    V3 oc = sub(r.o, c);
+    float a = dot(r.d, r.d);
+    float b = dot(oc, r.d);
+    float cc = dot(oc, oc) - rad * rad;
+    float disc = b * b - a * cc;
+    if (disc > 0) {
+        float t = (-b - sqrtf(disc)) / a;
+        if (t < RT_FLT_MAX && t > tmin) return t;
+        t = (-b + sqrtf(disc)) / a;
+        if (t < RT_FLT_MAX && t > tmin) return t;
+    }
+    return RT_INF;
+}
+
+__device__ __forceinline__ V3 msphere_center(float4 g0, float4 g1, float4 g2, float time) {   // sphere.h:81-83
+    return add(mk(g0.x, g0.y, g0.z), scale((time - g1.w) / g2.x, mk(g1.x, g1.y, g1.z)));
+}
+
+__device__ __forceinline__ float rect_t(int axis, float4 g0, float k, const Ray &r, float tmin) {   // aarect.h:50-100
+    float oa = axis == 0 ? r.o.x : (axis == 1 ? r.o.y : r.o.z);
+    float da = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
+    float t = (k - oa) / da;
+    if (t < tmin || t > RT_FLT_MAX) return RT_INF;
+    // in-plane axes: xy -> (x, y); xz -> (x, z); yz -> (y, z)
+    float oi = axis == 0 ? r.o.y : r.o.x, di = axis == 0 ? r.d.y : r.d.x;
+    float oj = axis == 2 ? r.o.y : r.o.z, dj = axis == 2 ? r.d.y : r.d.z;
+    float a = oi + t * di;
+    float b = oj + t * dj;
+    if (a < g0.x || a > g0.y || b < g0.z || b > g0.w) return RT_INF;
+    return t;
+}
+
+// prim kinds: 0 sphere, 1 moving sphere, 2 xy, 3 xz, 4 yz  (rect axis = 2, 1, 0)
+__device__ __forceinline__ int rect_axis(int kind) { return 4 - kind; }
+
+__device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float tmin,
+                                        int &key) {
+    const float4 g0 = P[idx * 4 + 0];
+    const float4 g1 = P[idx * 4 + 1];
+    const float4 g2 = P[idx * 4 + 2];
+    const float4 mm = P[idx * 4 + 3];
+    int kind = fbits(mm.x) & 0xff;
+    int inst = fbits(mm.z);
+    int order = fbits(mm.w);
+    Ray r = r0;
+    if (inst >= 0) r = to_object(insts, inst, r0);
+    float t;
+    if (kind == RT_PRIM_SPHERE) {
+        t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, r, tmin);
+        key = order;
+    } else if (kind == RT_PRIM_MOVING_SPHERE) {
+        t = sphere_t(msphere_center(g0, g1, g2, r.time), g0.w, r, tmin);
+        key = order;
+    } else {
+        t = rect_t(rect_axis(kind), g0, g1.x, r, tmin);
+        key = -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
+    }
+    return t;
+}
+
+struct Hit { V3 p, n; int mat; };
+
+// Rebuilds the reference's hit_record for the winning primitive (sphere.h:34-38,
+// 103-106; aarect.h:58-63; hitable.h:43-45, 69, 137-145).
+__device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float t) {
+    const float4 g0 = P[idx * 4 + 0];
+    const float4 g1 = P[idx * 4 + 1];
+    const float4 g2 = P[idx * 4 + 2];
+    const float4 mm = P[idx * 4 + 3];
+    int kind = fbits(mm.x) & 0xff;
+    int flip = (fbits(mm.x) >> 8) & 1;
+    int inst = fbits(mm.z);
+    Ray r = r0;
+    if (inst >= 0) r = to_object(insts, inst, r0);
+    Hit h;
+    h.p = at(r, t);
+    if (kind == RT_PRIM_SPHERE) {
+        h.n = divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w);
+    } else if (kind == RT_PRIM_MOVING_SPHERE) {
+        h.n = divs(sub(h.p, msphere_center(g0, g1, g2, r.time)), g0.w);
+    } else {
+        int axis = rect_axis(kind);
+        h.n = mk(axis == 0 ? 1.f : 0.f, axis == 1 ? 1.f : 0.f, axis == 2 ? 1.f : 0.f);
+    }
+    if (flip) h.n = neg(h.n);
+    if (inst >= 0) to_world(insts, inst, h.p, h.n);
+    h.mat = fbits(mm.y);
+    return h;
+}
+
+// Closest boundary hit of a constant_medium (its own small list), t > / >= tmin.
+__device__ __forceinline__ float boundary_t(const float4 *B, const float4 *insts, int first, int count, const Ray &r,
+                                            float tmin) {
+    float best = RT_INF;
+    for (int q = 0; q < count; ++q) {
+        int key;
+        float t = prim_t(B, insts, (uint32_t)(first + q), r, tmin, key);
+        if (t < best) best = t;
+    }
+    return best;
+}
+
+// ----------------------------------------------------------------- Perlin
+__device__ float perlin_noise(const float4 *ranvec, const int *perm, V3 p) {   // perlin.h:43-61, 25-39
+    float u = p.x - floorf(p.x);
+    float v = p.y - floorf(p.y);
+    float w = p.z - floorf(p.z);
+    u = u * u * (3 - 2 * u);
+    v = v * v * (3 - 2 * v);
+    w = w * w * (3 - 2 * w);
+    int i = (int)floorf(p.x);
+    int j = (int)floorf(p.y);
+    int k = (int)floorf(p.z);
+    float uu = u * u * (3 - 2 * u);
+    float vv = v * v * (3 - 2 * v);
+    float ww = w * w * (3 - 2 * w);
+    float accum = 0;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int d = 0; d < 2; d++) {
+                int h = perm[(i + a) & 255] ^ perm[256 + ((j + b) & 255)] ^ perm[512 + ((k + d) & 255)];
+                float4 g = ranvec[h];
+                V3 weight_v = mk(u - a, v - b, w - d);
+                accum += (a * uu + (1 - a) * (1 - uu)) * (b * vv + (1 - b) * (1 - vv)) *
+                         (d * ww + (1 - d) * (1 - ww)) * dot(mk(g.x, g.y, g.z), weight_v);
+            }
+    return accum;
+}
+
+__device__ float perlin_turb(const float4 *ranvec, const int *perm, V3 p) {   // perlin.h:64-74
+    float accum = 0;
+    V3 temp_p = p;
+    float weight = 1.0f;
+    for (int i = 0; i < 7; i++) {
+        accum += weight * perlin_noise(ranvec, perm, temp_p);
+        weight = (float)((double)weight * 0.5);
+        temp_p = mk(temp_p.x * 2, temp_p.y * 2, temp_p.z * 2);
+    }
+    return fabsf(accum);
+}
+
+template <bool kCount>
+__device__ V3 tex_value(const RtKernelArgs &A, int ti, V3 p, uint64_t &noise_cnt) {   // texture.h:16-59
+    for (int guard = 0; guard < RT_MAX_CHECKER_DEPTH; ++guard) {
+        const float4 t0 = A.texs[ti * 2 + 0];
+        const float4 t1 = A.texs[ti * 2 + 1];
+        int kind = fbits(t0.x);
+        if (kind == RT_TEX_CONSTANT) return mk(t1.x, t1.y, t1.z);
+        if (kind == RT_TEX_CHECKER) {
+            float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+            ti = (sines < 0) ? fbits(t0.z) : fbits(t0.y);
+            continue;
+        }
+        // RT_TEX_NOISE
+        if (kCount) noise_cnt++;
+        float sc = t0.w;
+        float s = 1 + sinf(sc * p.x + 5 * perlin_turb(A.ranvec, A.perm, scale(sc, p)));
+        float h = 0.5f * 1;
+        return mk(s * h, s * h, s * h);
+    }
+    return mk(0, 0, 0);
+}
+
+// --------------------------------------------------------------- scatter
+__device__ __forceinline__ V3 random_in_unit_sphere(Rng &g) {   // material.h:41-47
+    V3 p;
+    do {
+        double x = g.next(), y = g.next(), z = g.next();
+        p = sub(scale(2.0f, mk((float)x, (float)y, (float)z)), mk(1, 1, 1));
+    } while ((double)dot(p, p) >= 1.0);
+    return p;
+}
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(2 * dot(v, n), n)); }   // material.h:36-38
+
+// ------------------------------------------------------------ work claim
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
+
+template <bool kCount>
+__global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
+    __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
+    const uint32_t lane = lane_id();
+    uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
+
+    // wave-uniform claim pool
+    uint32_t pool_next = 0, pool_end = 0;
+    bool exhausted = false;
+
+    // lane state
+    uint32_t item = 0xFFFFFFFFu;
+    int s_cur = 0, s_end = 0;
+    V3 part = mk(0, 0, 0);
+    bool path = false, finished = false;
+    Ray r;
+    r.o = mk(0, 0, 0); r.d = mk(0, 0, 0); r.time = 0;
+    V3 beta = mk(1, 1, 1);
+    int depth = 0;
+    Rng g; g.key = 0; g.n = 0;
+    uint32_t px = 0, py = 0;
+
+    uint64_t c_samples = 0, c_segments = 0, c_nodes = 0, c_prims = 0, c_media = 0, c_noise = 0, c_inst = 0;
+
+
+    for (;;) {
+        // ---- 1. retire a finished work item, claim new ones ------------------
+        if (!path && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
+            A.slab[item] = make_float4(part.x, part.y, part.z, 0.f);
+            item = 0xFFFFFFFFu;
+        }
+        bool need = !path && !finished && item == 0xFFFFFFFFu;
+        uint64_t need_mask = __ballot(need);
+        while (need_mask != 0ull && !exhausted) {
+            if (pool_next == pool_end) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(A.counter, kClaim);
+                base = __shfl(base, 0);
+                if (base >= A.nitems) { exhausted = true; break; }
+                pool_next = base;
+                pool_end = min(base + kClaim, A.nitems);
+            }
+            uint32_t avail = pool_end - pool_next;
+            uint32_t rank = lanes_below(need_mask);
+            if (need && rank < avail) {
+                item = pool_next + rank;
+                need = false;
+                uint32_t c = item / A.npix;
+                uint32_t p = item - c * A.npix;
+                uint32_t xy = A.job_xy[p];
+                px = xy & 0xFFFFu;
+                py = xy >> 16;
+                s_cur = (int)(c * (uint32_t)A.chunk);
+                s_end = min(s_cur + A.chunk, A.ns);
+                part = mk(0, 0, 0);
+            }
+            uint32_t wanted = (uint32_t)__popcll(need_mask);
+            pool_next += min(wanted, avail);
+            need_mask = __ballot(need);
+        }
+        if (need) finished = true;
+        if (__ballot(!finished) == 0ull) break;
+
+        // ---- 2. start a camera sample (main.cpp:305-308, camera.h:41-56) -----
+        if (!path && !finished) {
+            int j = A.ny - 1 - (int)py;
+            g.key = sample_key(A.seed, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset);
+            g.n = 0;
+            float u = (float)((double)(int)px + g.next()) / (float)A.nx;
+            float v = (float)((double)j + g.next()) / (float)A.ny;
+            V3 p;
+            do {
+                double a = g.next(), b = g.next();
+                p = sub(scale(2.0f, mk((float)a, (float)b, 0)), mk(1, 1, 0));
+            } while ((double)dot(p, p) >= 1.0);
+            V3 rd = scale(A.lens, p);
+            V3 cu = mk(A.cu[0], A.cu[1], A.cu[2]), cv = mk(A.cv[0], A.cv[1], A.cv[2]);
+            V3 offset = add(scale(rd.x, cu), scale(rd.y, cv));
+            float time = (float)((double)A.ct0 + g.next() * (double)(A.ct1 - A.ct0));
+            V3 org = mk(A.org[0], A.org[1], A.org[2]);
+            V3 dir = sub(sub(add(add(mk(A.llc[0], A.llc[1], A.llc[2]), scale(u, mk(A.hor[0], A.hor[1], A.hor[2]))),
+                                 scale(v, mk(A.ver[0], A.ver[1], A.ver[2]))), org), offset);
+            r.o = add(org, offset);
+            r.d = dir;
+            r.time = time;
+            beta = mk(1, 1, 1);
+            depth = 0;
+            path = true;
+            if (kCount) c_samples++;
+        }
+
+        if (!path) continue;   // finished lanes idle until the wave drains
+
+        // ---- 3. closest surface hit: BVH2, stack in LDS ------------------------
+        if (kCount) c_segments++;
+        float best_t = RT_FLT_MAX;
+        int best_key = 0x7FFFFFFF;
+        uint32_t best_prim = 0xFFFFFFFFu;
+        if (A.has_bvh) {
+            const float ix = 1.0f / r.d.x, iy = 1.0f / r.d.y, iz = 1.0f / r.d.z;
+            const float nox = -r.o.x * ix, noy = -r.o.y * iy, noz = -r.o.z * iz;
+            uint32_t node = A.root;
+            int sp = 0;
+            for (;;) {
+                if (!(node & RT_LEAF_BIT)) {
+                    if (kCount) c_nodes++;
+                    const float4 b0 = A.nodes[node * 4 + 0];
+                    const float4 b1 = A.nodes[node * 4 + 1];
+                    const float4 b2 = A.nodes[node * 4 + 2];
+                    const float4 cf = A.nodes[node * 4 + 3];
+                    const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
+                    float a0 = __builtin_fmaf(b0.x, ix, nox), a1 = __builtin_fmaf(b0.y, ix, nox);
+                    float a2 = __builtin_fmaf(b0.z, iy, noy), a3 = __builtin_fmaf(b0.w, iy, noy);
+                    float a4 = __builtin_fmaf(b1.x, iz, noz), a5 = __builtin_fmaf(b1.y, iz, noz);
+                    float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), A.tmin));
+                    float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), best_t));
+                    float e0 = __builtin_fmaf(b1.z, ix, nox), e1 = __builtin_fmaf(b1.w, ix, nox);
+                    float e2 = __builtin_fmaf(b2.x, iy, noy), e3 = __builtin_fmaf(b2.y, iy, noy);
+                    float e4 = __builtin_fmaf(b2.z, iz, noz), e5 = __builtin_fmaf(b2.w, iz, noz);
+                    float tn1 = fmaxf(fmaxf(fminf(e0, e1), fminf(e2, e3)), fmaxf(fminf(e4, e5), A.tmin));
+                    float tf1 = fminf(fminf(fmaxf(e0, e1), fmaxf(e2, e3)), fminf(fmaxf(e4, e5), best_t));
+                    bool h0 = tn0 <= tf0 && c0 != RT_EMPTY_CHILD;
+                    bool h1 = tn1 <= tf1 && c1 != RT_EMPTY_CHILD;
+                    if (h0 && h1) {
+                        uint32_t nearc = c0, farc = c1;
+                        if (tn1 < tn0) { nearc = c1; farc = c0; }
+                        stk[sp * 64] = farc;
+                        ++sp;
+                        node = nearc;
+                        continue;
+                    }
+                    if (h0) { node = c0; continue; }
+                    if (h1) { node = c1; continue; }
+                } else {
+                    const uint32_t first = RT_LEAF_FIRST(node), cnt = RT_LEAF_COUNT(node);
+                    for (uint32_t q = 0; q < cnt; ++q) {
+                        int key;
+                        float t = prim_t(A.prims, A.insts, first + q, r, A.tmin, key);
+                        if (kCount) c_prims++;
+                        if (t < best_t || (t == best_t && key < best_key)) {
+                            best_t = t; best_key = key; best_prim = first + q;
+                        }
+                    }
+                }
+                if (sp == 0) break;
+                --sp;
+                node = stk[sp * 64];
+            }
+        }
+
+        // ---- 4. media after the surfaces (constant_medium.h:26-50) -------------
+        bool have = best_prim != 0xFFFFFFFFu;
+        Hit hr;
+        if (have) hr = prim_record(A.prims, A.insts, best_prim, r, best_t);
+        for (int k = 0; k < A.nmedia; ++k) {
+            if (kCount) c_media++;
+            const int4 md = A.media[k];
+            float r1 = boundary_t(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX);
+            if (r1 == RT_INF) continue;
+            float r2 = boundary_t(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001));
+            if (r2 == RT_INF) continue;
+            float tmax = have ? best_t : RT_FLT_MAX;
+            if (r1 < A.tmin) r1 = A.tmin;
+            if (r2 > tmax) r2 = tmax;
+            if (r1 >= r2) continue;
+            if (r1 < 0) r1 = 0;
+            float dlen = len(r.d);
+            float distance_inside_boundary = (r2 - r1) * dlen;
+            float density = __int_as_float(md.z);
+            float hit_distance = (float)((double)(-(1 / density)) * log(g.medium(depth, k)));
+            if (hit_distance < distance_inside_boundary) {
+                best_t = r1 + hit_distance / dlen;
+                have = true;
+                hr.p = at(r, best_t);
+                hr.n = mk(1, 0, 0);
+                hr.mat = md.w;
+            }
+        }
+
+        // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
+        V3 L;
+        bool terminate = true;
+        if (!have) {
+            if (A.background == RT_BG_SKY) {                                  // TNW/Chapter03:29-31
+                V3 ud = unit(r.d);
+                float t = (float)(0.5 * ((double)ud.y + 1.0));
+                V3 sky = add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
+                L = mul(beta, sky);
+            } else {
+                L = mul(beta, mk(0, 0, 0));
+            }
+        } else {
+            const float4 m0 = A.mats[hr.mat * 2 + 0];
+            const float4 m1 = A.mats[hr.mat * 2 + 1];
+            const int kind = fbits(m0.x);
+            const int tex = fbits(m0.y);
+            V3 emitted = mk(0, 0, 0);
+            if (kind == RT_MAT_DIFFUSE_LIGHT) emitted = tex_value<kCount>(A, tex, hr.p, c_noise);
+            bool scattered = false;
+            V3 att = mk(0, 0, 0);
+            Ray ns;
+            if (depth < A.max_depth) {
+                if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
+                    V3 target = add(add(hr.p, hr.n), random_in_unit_sphere(g));
+                    ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
+                    att = tex_value<kCount>(A, tex, hr.p, c_noise);
+                    scattered = true;
+                } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
+                    V3 reflected = reflect(unit(r.d), hr.n);
+                    ns.o = hr.p; ns.d = add(reflected, scale(m0.z, random_in_unit_sphere(g))); ns.time = 0.0f;
+                    att = mk(m1.x, m1.y, m1.z);
+                    scattered = dot(ns.d, hr.n) > 0;
+                } else if (kind == RT_MAT_DIELECTRIC) {                       // material.h:90-120
+                    const float ref_idx = m0.w;
+                    V3 outward_normal;
+                    V3 reflected = reflect(r.d, hr.n);
+                    float ni_over_nt, cosine;
+                    att = mk(1.0f, 1.0f, 1.0f);
+                    float dn = dot(r.d, hr.n);
+                    if (dn > 0) {
+                        outward_normal = neg(hr.n);
+                        ni_over_nt = ref_idx;
+                        cosine = dot(r.d, hr.n) / len(r.d);
+                        cosine = sqrtf(1 - ref_idx * ref_idx * (1 - cosine * cosine));
+                    } else {
+                        outward_normal = hr.n;
+                        ni_over_nt = (float)(1.0 / (double)ref_idx);
+                        cosine = -dot(r.d, hr.n) / len(r.d);
+                    }
+                    // refract, material.h:23-33
+                    V3 uv = unit(r.d);
+                    float dt = dot(uv, outward_normal);
+                    float disc = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
+                    float reflect_prob;
+                    V3 refracted = mk(0, 0, 0);
+                    if (disc > 0) {
+                        refracted = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))),
+                                        scale(sqrtf(disc), outward_normal));
+                        // schlick, material.h:16-20
+                        float r0 = (1 - ref_idx) / (1 + ref_idx);
+                        r0 = r0 * r0;
+                        reflect_prob = (float)(r0 + (double)(1 - r0) * pow((double)(1 - cosine), 5.0));
+                    } else {
+                        reflect_prob = 1.0f;
+                    }
+                    ns.o = hr.p; ns.time = 0.0f;
+                    ns.d = (g.next() < (double)reflect_prob) ? reflected : refracted;
+                    scattered = true;
+                } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
+                    ns.o = hr.p; ns.d = random_in_unit_sphere(g); ns.time = 0.0f;
+                    att = tex_value<kCount>(A, tex, hr.p, c_noise);
+                    scattered = true;
+                }
+            }
+            if (scattered) {
+                beta = mul(beta, att);
+                r = ns;
+                ++depth;
+                terminate = false;
+            } else {
+                L = mul(beta, emitted);
+            }
+        }
+        if (terminate) {
+            if (!(L.x == L.x)) L.x = 0;                                       // de_nan, main.cpp:232-242
+            if (!(L.y == L.y)) L.y = 0;
+            if (!(L.z == L.z)) L.z = 0;
+            part = add(part, L);
+            ++s_cur;
+            path = false;
+        }
+    }
+
+    if (kCount) {
+        uint64_t v[RT_CNT_N] = {c_samples, c_segments, c_nodes, c_prims, c_media, c_noise, 0, c_inst};
+        for (int k = 0; k < RT_CNT_N; ++k) {
+            uint64_t x = v[k];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+            if (lane == 0 && x) atomicAdd(&A.stats[k], (unsigned long long)x);
+        }
+    }
+}
+
+// Sums each pixel's chunk partials in chunk order and applies `col /= float(ns)`
+// (vec3.h:134-141: multiply by float(1.0/ns)).
+__global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ slab, uint32_t npix, int nchunks, float k,
+                                                  const uint32_t *__restrict__ out_index, float *__restrict__ out) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    V3 col = mk(0, 0, 0);
+    for (int c = 0; c < nchunks; ++c) {
+        float4 v = slab[(size_t)c * npix + p];
+        col = add(col, mk(v.x, v.y, v.z));
+    }
+    uint32_t o = out_index[p];
+    out[3 * (size_t)o + 0] = col.x * k;
+    out[3 * (size_t)o + 1] = col.y * k;
+    out[3 * (size_t)o + 2] = col.z * k;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------- launchers
+extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, bool count, hipStream_t stream) {
+    if (count)
+        hipLaunchKernelGGL(rt_megakernel<true>, dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+    else
+        hipLaunchKernelGGL(rt_megakernel<false>, dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, const uint32_t *out_index,
+                                        float *out, hipStream_t stream) {
+    int blocks = (int)((npix + 255) / 256);
+    hipLaunchKernelGGL(rt_resolve, dim3(blocks), dim3(256), 0, stream, slab, npix, nchunks, k, out_index, out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, bool count) {
+    if (count)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false>, RT_BLOCK, 0);
+}

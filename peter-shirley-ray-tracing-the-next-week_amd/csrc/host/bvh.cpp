@@ -1,0 +1,266 @@
+// bvh.cpp — binned-SAH BVH2 over the flattened surface primitives.
+//
+// Replaces the reference's bvh_node construction (bvh.h:97-121: random axis,
+// median split, recursive) with a surface-area-heuristic build, and its buggy
+// slab test (aabb.h:38-39) with a correct one on the device.  Because the device
+// breaks ties by list order, the traversal returns the same hit as the flat
+// list whatever the tree shape, so the build is a pure performance choice.
+//
+// Boxes are conservative: every primitive box is padded by an absolute plus a
+// relative margin, so a hit the primitive test accepts can never lie outside the
+// boxes on its path.
+#include "bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+
+namespace rtnw {
+
+namespace {
+
+struct Box {
+    double lo[3], hi[3];
+    Box() { for (int k = 0; k < 3; k++) { lo[k] = 1e300; hi[k] = -1e300; } }
+    void grow(const double p[3]) { for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); } }
+    void grow(const Box &b) { for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); } }
+    bool valid() const { return lo[0] <= hi[0]; }
+    double area() const {
+        if (!valid()) return 0;
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return 2 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+// World-space box of one primitive, through its instance chain (outermost first).
+Box prim_box(const rt_prim &p, const rt_instance *instances, double ta, double tb) {
+    Box b;
+    const float *q = p.p;
+    auto add_sphere = [&](double cx, double cy, double cz, double r) {
+        r = std::fabs(r);
+        const double lo[3] = {cx - r, cy - r, cz - r}, hi[3] = {cx + r, cy + r, cz + r};
+        b.grow(lo);
+        b.grow(hi);
+    };
+    switch (p.kind) {
+    case RT_PRIM_SPHERE: add_sphere(q[0], q[1], q[2], q[3]); break;
+    case RT_PRIM_MOVING_SPHERE: {
+        const double span = (double)q[7] - (double)q[6];
+        for (double t : {ta, tb}) {
+            const double s = span != 0 ? (t - q[6]) / span : 0.0;
+            add_sphere(q[0] + s * (q[3] - q[0]), q[1] + s * (q[4] - q[1]), q[2] + s * (q[5] - q[2]), q[8]);
+        }
+        break;
+    }
+    case RT_PRIM_XY_RECT: { const double lo[3] = {q[0], q[2], q[4]}, hi[3] = {q[1], q[3], q[4]}; b.grow(lo); b.grow(hi); break; }
+    case RT_PRIM_XZ_RECT: { const double lo[3] = {q[0], q[4], q[2]}, hi[3] = {q[1], q[4], q[3]}; b.grow(lo); b.grow(hi); break; }
+    case RT_PRIM_YZ_RECT: { const double lo[3] = {q[4], q[0], q[2]}, hi[3] = {q[4], q[1], q[3]}; b.grow(lo); b.grow(hi); break; }
+    default: throw std::runtime_error("unknown primitive kind");
+    }
+    if (p.instance >= 0) {
+        const rt_instance &in = instances[p.instance];
+        for (int k = in.nops - 1; k >= 0; --k) {   // object -> world, innermost wrapper first
+            const int op = (int)in.ops[k][0];
+            Box w;
+            for (int c = 0; c < 8; c++) {
+                double v[3] = {(c & 1) ? b.hi[0] : b.lo[0], (c & 2) ? b.hi[1] : b.lo[1], (c & 4) ? b.hi[2] : b.lo[2]};
+                if (op == RT_OP_TRANSLATE) {
+                    for (int a = 0; a < 3; a++) v[a] += in.ops[k][1 + a];
+                } else if (op == RT_OP_ROTATE_Y) {
+                    const double s = in.ops[k][1], co = in.ops[k][2];
+                    const double x = co * v[0] + s * v[2], z = -s * v[0] + co * v[2];
+                    v[0] = x;
+                    v[2] = z;
+                }
+                w.grow(v);
+            }
+            b = w;
+        }
+    }
+    // conservative margin: 1e-3 absolute + 1e-4 of the coordinate magnitude
+    for (int k = 0; k < 3; k++) {
+        const double mag = std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k]));
+        const double pad = 1e-3 + 1e-4 * mag;
+        b.lo[k] -= pad;
+        b.hi[k] += pad;
+    }
+    return b;
+}
+
+struct Item {
+    Box box;
+    double c[3];
+    int idx;
+};
+
+struct Builder {
+    std::vector<Item> items;
+    std::vector<rt_dnode> nodes;
+    std::vector<int> order;   // leaf order -> original prim index
+    int max_depth_seen = 0;
+
+    uint32_t leaf(int begin, int end) {
+        const uint32_t first = (uint32_t)order.size();
+        for (int i = begin; i < end; i++) order.push_back(items[i].idx);
+        return RT_LEAF_REF(first, end - begin);
+    }
+
+    static void put_box(rt_dnode &n, int child, const Box &b) {
+        const float lo[3] = {(float)b.lo[0], (float)b.lo[1], (float)b.lo[2]};
+        const float hi[3] = {(float)b.hi[0], (float)b.hi[1], (float)b.hi[2]};
+        // round outward so the float box contains the double box
+        float flo[3], fhi[3];
+        for (int k = 0; k < 3; k++) {
+            flo[k] = ((double)lo[k] > b.lo[k]) ? std::nextafter(lo[k], -INFINITY) : lo[k];
+            fhi[k] = ((double)hi[k] < b.hi[k]) ? std::nextafter(hi[k], INFINITY) : hi[k];
+        }
+        if (child == 0) {
+            n.b0[0] = flo[0]; n.b0[1] = fhi[0]; n.b0[2] = flo[1]; n.b0[3] = fhi[1];
+            n.b1[0] = flo[2]; n.b1[1] = fhi[2];
+        } else {
+            n.b1[2] = flo[0]; n.b1[3] = fhi[0];
+            n.b2[0] = flo[1]; n.b2[1] = fhi[1]; n.b2[2] = flo[2]; n.b2[3] = fhi[2];
+        }
+    }
+
+    Box range_box(int begin, int end) const {
+        Box b;
+        for (int i = begin; i < end; i++) b.grow(items[i].box);
+        return b;
+    }
+
+    // Returns the split position in [begin, end) or -1 to make a leaf.
+    int split(int begin, int end, int depth) {
+        const int n = end - begin;
+        // depth budget: a median split from here must still fit RT_MAX_BVH_DEPTH
+        int need = 0;
+        for (int m = n; m > 4; m = (m + 1) / 2) need++;
+        const bool force_median = depth + need + 1 >= RT_MAX_BVH_DEPTH;
+        if (n <= 2 && !force_median) return -1;
+
+        Box cb;
+        for (int i = begin; i < end; i++) cb.grow(items[i].c);
+        int axis = 0;
+        double ext = -1;
+        for (int k = 0; k < 3; k++) if (cb.hi[k] - cb.lo[k] > ext) { ext = cb.hi[k] - cb.lo[k]; axis = k; }
+
+        if (force_median || ext <= 0) {
+            if (n <= RT_MAX_LEAF && !force_median) return -1;
+            if (n <= 4) return -1;
+            const int mid = begin + n / 2;
+            std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
+                             [axis](const Item &a, const Item &b) { return a.c[axis] < b.c[axis]; });
+            return mid;
+        }
+
+        constexpr int kBins = 32;
+        const double parent_area = range_box(begin, end).area();
+        double best_cost = 1e300;
+        int best_axis = -1, best_bin = -1;
+        for (int k = 0; k < 3; k++) {
+            const double e = cb.hi[k] - cb.lo[k];
+            if (e <= 0) continue;
+            Box bins[kBins];
+            int counts[kBins] = {0};
+            for (int i = begin; i < end; i++) {
+                int bi = (int)((items[i].c[k] - cb.lo[k]) / e * kBins);
+                bi = std::min(std::max(bi, 0), kBins - 1);
+                counts[bi]++;
+                bins[bi].grow(items[i].box);
+            }
+            double right_area[kBins];
+            int right_count[kBins];
+            Box acc;
+            int cnt = 0;
+            for (int b = kBins - 1; b > 0; b--) {
+                acc.grow(bins[b]);
+                cnt += counts[b];
+                right_area[b] = acc.area();
+                right_count[b] = cnt;
+            }
+            Box lacc;
+            int lcnt = 0;
+            for (int b = 1; b < kBins; b++) {
+                lacc.grow(bins[b - 1]);
+                lcnt += counts[b - 1];
+                if (lcnt == 0 || right_count[b] == 0) continue;
+                const double cost = 1.0 + (lacc.area() * lcnt + right_area[b] * right_count[b]) / parent_area;
+                if (cost < best_cost) { best_cost = cost; best_axis = k; best_bin = b; }
+            }
+        }
+        const double leaf_cost = (double)n;
+        if (best_axis < 0 || (best_cost >= leaf_cost && n <= RT_MAX_LEAF)) {
+            if (n <= RT_MAX_LEAF) return -1;
+            const int mid = begin + n / 2;
+            std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
+                             [axis](const Item &a, const Item &b) { return a.c[axis] < b.c[axis]; });
+            return mid;
+        }
+        const double lo = cb.lo[best_axis], e = cb.hi[best_axis] - cb.lo[best_axis];
+        auto mid_it = std::partition(items.begin() + begin, items.begin() + end, [&](const Item &it) {
+            int bi = (int)((it.c[best_axis] - lo) / e * kBins);
+            bi = std::min(std::max(bi, 0), kBins - 1);
+            return bi < best_bin;
+        });
+        int mid = (int)(mid_it - items.begin());
+        if (mid == begin || mid == end) mid = begin + n / 2;
+        return mid;
+    }
+
+    // Builds the subtree over [begin, end); returns its child reference.
+    uint32_t build(int begin, int end, int depth) {
+        const int s = split(begin, end, depth);
+        if (s < 0) {
+            if (end - begin > RT_MAX_LEAF) throw std::runtime_error("bvh: leaf too large");
+            return leaf(begin, end);
+        }
+        const uint32_t id = (uint32_t)nodes.size();
+        nodes.push_back(rt_dnode{});
+        max_depth_seen = std::max(max_depth_seen, depth + 1);
+        if (depth + 1 > RT_MAX_BVH_DEPTH) throw std::runtime_error("bvh: depth budget exceeded");
+        const Box lb = range_box(begin, s), rb = range_box(s, end);
+        const uint32_t l = build(begin, s, depth + 1);
+        const uint32_t r = build(s, end, depth + 1);
+        rt_dnode &n = nodes[id];
+        put_box(n, 0, lb);
+        put_box(n, 1, rb);
+        n.ch[0] = l;
+        n.ch[1] = r;
+        n.ch[2] = n.ch[3] = 0;
+        return id;
+    }
+};
+
+}  // namespace
+
+BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, float time0, float time1) {
+    BvhResult res;
+    if (n <= 0) return res;
+    const double ta = std::min(0.0, (double)time0), tb = std::max(0.0, (double)time1);
+    Builder b;
+    b.items.resize(n);
+    for (int i = 0; i < n; i++) {
+        Item &it = b.items[i];
+        it.box = prim_box(prims[i], instances, ta, tb);
+        for (int k = 0; k < 3; k++) it.c[k] = 0.5 * (it.box.lo[k] + it.box.hi[k]);
+        it.idx = i;
+    }
+    const uint32_t root = b.build(0, n, 0);
+    if (root & RT_LEAF_BIT) {   // tiny scene: wrap the single leaf in a root node
+        rt_dnode r{};
+        Builder::put_box(r, 0, b.range_box(0, n));
+        r.ch[0] = root;
+        r.ch[1] = RT_EMPTY_CHILD;
+        b.nodes.push_back(r);
+        res.root = (uint32_t)b.nodes.size() - 1;
+        res.depth = 1;
+    } else {
+        res.root = 0;
+        res.depth = b.max_depth_seen;
+    }
+    res.nodes = std::move(b.nodes);
+    res.order = std::move(b.order);
+    return res;
+}
+
+}  // namespace rtnw

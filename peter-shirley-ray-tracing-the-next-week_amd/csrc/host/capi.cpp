@@ -1,0 +1,526 @@
+// capi.cpp — the C ABI of librt_hip.so (include/rt_hip.h): scene upload to HBM,
+// job setup, megakernel + resolve launches, timing, and host helpers.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rt_hip.h"
+#include "../rt_layout.h"
+#include "../hip/rt_kernel.h"
+#include "bvh.h"
+#include "rtnw.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char *what) {
+    return fail(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+template <class T>
+int upload(void **dst, const std::vector<T> &v) {
+    *dst = nullptr;
+    if (v.empty()) return RT_OK;
+    HIP_TRY(hipMalloc(dst, v.size() * sizeof(T)));
+    HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+int ibits(float f) { int i; std::memcpy(&i, &f, 4); return i; }
+float fbits(int i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+rt_dprim to_dprim(const rt_prim &p, int order) {
+    rt_dprim d{};
+    const float *q = p.p;
+    switch (p.kind) {
+    case RT_PRIM_SPHERE:
+        d.g0[0] = q[0]; d.g0[1] = q[1]; d.g0[2] = q[2]; d.g0[3] = q[3];
+        break;
+    case RT_PRIM_MOVING_SPHERE:
+        // center(t) = c0 + ((t - t0) / (t1 - t0)) * (c1 - c0): the two differences
+        // are float subtractions of the reference (sphere.h:82), computed once here.
+        d.g0[0] = q[0]; d.g0[1] = q[1]; d.g0[2] = q[2]; d.g0[3] = q[8];
+        d.g1[0] = q[3] - q[0]; d.g1[1] = q[4] - q[1]; d.g1[2] = q[5] - q[2]; d.g1[3] = q[6];
+        d.g2[0] = q[7] - q[6];
+        break;
+    default:   // rects
+        d.g0[0] = q[0]; d.g0[1] = q[1]; d.g0[2] = q[2]; d.g0[3] = q[3];
+        d.g1[0] = q[4];
+        break;
+    }
+    d.m[0] = p.kind | (p.flip ? 1 << 8 : 0);
+    d.m[1] = p.material;
+    d.m[2] = p.instance;
+    d.m[3] = order;
+    return d;
+}
+
+}  // namespace
+
+struct rt_scene {
+    int device = 0;
+    int cus = 0;
+    int grid = 0, grid_count = 0;
+    hipStream_t own_stream = nullptr;
+    // scene in HBM
+    void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
+         *insts = nullptr, *ranvec = nullptr, *perm = nullptr;
+    uint32_t root = 0;
+    int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0;
+    bool has_moving = false;
+    float time0 = 0, time1 = 1;
+    // job cache
+    std::vector<int32_t> job_tiles;
+    uint32_t npix = 0;
+    void *job_xy = nullptr, *job_out = nullptr;
+    void *slab = nullptr;
+    size_t slab_bytes = 0;
+    void *counter = nullptr, *stats = nullptr;
+    void *host_out = nullptr;
+    size_t host_out_bytes = 0;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
+
+extern "C" {
+
+const char *rt_last_error(void) { return g_err.c_str(); }
+const char *rt_version(void) { return "rt_hip 1 (gfx950 persistent megakernel)"; }
+
+int rt_device_count(int *out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *out = 0; return hip_fail(e, "hipGetDeviceCount"); }
+    *out = n;
+    return RT_OK;
+}
+
+int rt_device_alloc(int device, uint64_t bytes, void **out) {
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipMalloc(out, bytes));
+    return RT_OK;
+}
+int rt_device_free(void *ptr) {
+    HIP_TRY(hipFree(ptr));
+    return RT_OK;
+}
+int rt_copy_to_host(void *dst, const void *src, uint64_t bytes) {
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_camera_init(rt_camera_desc *out, const float lookfrom[3], const float lookat[3], const float vup[3], float vfov,
+                   float aspect, float aperture, float focus_dist, float t0, float t1) {
+    if (!out || !lookfrom || !lookat || !vup) return fail(RT_ERR_INVALID, "rt_camera_init: null argument");
+    rtnw::camera c(rtnw::vec3(lookfrom[0], lookfrom[1], lookfrom[2]), rtnw::vec3(lookat[0], lookat[1], lookat[2]),
+                   rtnw::vec3(vup[0], vup[1], vup[2]), vfov, aspect, aperture, focus_dist, t0, t1);
+    *out = c.desc();
+    return RT_OK;
+}
+
+static int validate_desc(const rt_scene_desc *d) {
+    if (!d) return fail(RT_ERR_INVALID, "null scene descriptor");
+    if (d->abi_version != RT_ABI_VERSION) return fail(RT_ERR_INVALID, "rt_scene_desc.abi_version mismatch");
+    if (d->nprims < 0 || d->nboundary < 0 || d->nmedia < 0 || d->nmaterials < 0 || d->ntextures < 0 || d->ninstances < 0)
+        return fail(RT_ERR_INVALID, "negative count in scene descriptor");
+    if (d->nprims > (1 << 24) - 1 || d->nboundary > (1 << 24) - 1) return fail(RT_ERR_INVALID, "too many primitives");
+    if (!d->perlin_ranvec || !d->perlin_perm) return fail(RT_ERR_INVALID, "missing Perlin tables");
+    auto check_prim = [&](const rt_prim &p) -> int {
+        if (p.kind < RT_PRIM_SPHERE || p.kind > RT_PRIM_YZ_RECT) return fail(RT_ERR_INVALID, "bad primitive kind");
+        if (p.material < 0 || p.material >= d->nmaterials) return fail(RT_ERR_INVALID, "primitive material out of range");
+        if (p.instance < -1 || p.instance >= d->ninstances) return fail(RT_ERR_INVALID, "primitive instance out of range");
+        return RT_OK;
+    };
+    for (int i = 0; i < d->nprims; i++) if (int rc = check_prim(d->prims[i])) return rc;
+    for (int i = 0; i < d->nboundary; i++) if (int rc = check_prim(d->boundary_prims[i])) return rc;
+    for (int i = 0; i < d->nmedia; i++) {
+        const rt_medium &m = d->media[i];
+        if (m.boundary_first < 0 || m.boundary_count < 0 || m.boundary_first + m.boundary_count > d->nboundary)
+            return fail(RT_ERR_INVALID, "medium boundary range out of range");
+        if (m.material < 0 || m.material >= d->nmaterials) return fail(RT_ERR_INVALID, "medium material out of range");
+    }
+    for (int i = 0; i < d->ninstances; i++) {
+        const rt_instance &in = d->instances[i];
+        if (in.nops < 0 || in.nops > RT_MAX_INSTANCE_OPS) return fail(RT_ERR_INVALID, "instance chain too long");
+        for (int k = 0; k < in.nops; k++) {
+            const int op = (int)in.ops[k][0];
+            if (op < RT_OP_TRANSLATE || op > RT_OP_FLIP) return fail(RT_ERR_INVALID, "bad instance op");
+        }
+    }
+    for (int i = 0; i < d->ntextures; i++) {
+        const rt_texture &t = d->textures[i];
+        if (t.kind == RT_TEX_IMAGE) return fail(RT_ERR_UNSUPPORTED, "image_texture is not supported on the device yet");
+        if (t.kind < RT_TEX_CONSTANT || t.kind > RT_TEX_IMAGE) return fail(RT_ERR_INVALID, "bad texture kind");
+        if (t.kind == RT_TEX_CHECKER) {
+            if (t.even < 0 || t.even >= d->ntextures || t.odd < 0 || t.odd >= d->ntextures)
+                return fail(RT_ERR_INVALID, "checker child out of range");
+        }
+    }
+    // checker chains must terminate within the device's depth guard
+    for (int i = 0; i < d->ntextures; i++) {
+        std::vector<int> stack{i};
+        std::vector<int> depth{0};
+        while (!stack.empty()) {
+            int t = stack.back(), dd = depth.back();
+            stack.pop_back(); depth.pop_back();
+            if (dd >= RT_MAX_CHECKER_DEPTH) return fail(RT_ERR_UNSUPPORTED, "checker textures nested too deep (or cyclic)");
+            if (d->textures[t].kind == RT_TEX_CHECKER) {
+                stack.push_back(d->textures[t].even); depth.push_back(dd + 1);
+                stack.push_back(d->textures[t].odd); depth.push_back(dd + 1);
+            }
+        }
+    }
+    for (int i = 0; i < d->nmaterials; i++) {
+        const rt_material &m = d->materials[i];
+        if (m.kind < RT_MAT_LAMBERTIAN || m.kind > RT_MAT_ISOTROPIC) return fail(RT_ERR_INVALID, "bad material kind");
+        const bool textured = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_DIFFUSE_LIGHT || m.kind == RT_MAT_ISOTROPIC;
+        if (textured && (m.texture < 0 || m.texture >= d->ntextures)) return fail(RT_ERR_INVALID, "material texture out of range");
+    }
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene *s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    for (void *p : {s->nodes, s->prims, s->bprims, s->media, s->mats, s->texs, s->insts, s->ranvec, s->perm, s->job_xy,
+                    s->job_out, s->slab, s->counter, s->stats, s->host_out})
+        if (p) (void)hipFree(p);
+    for (auto &e : s->ev) if (e) (void)hipEventDestroy(e);
+    if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
+    delete s;
+}
+
+int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
+    if (!out) return fail(RT_ERR_INVALID, "rt_scene_create: null out");
+    *out = nullptr;
+    if (int rc = validate_desc(d)) return rc;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) return fail(RT_ERR_HIP, "no HIP device available (the path tracer has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+
+    rtnw::BvhResult bvh;
+    try {
+        bvh = rtnw::build_bvh(d->prims, d->nprims, d->instances, d->time0, d->time1);
+    } catch (const std::exception &ex) {
+        return fail(RT_ERR_INVALID, std::string("BVH build failed: ") + ex.what());
+    }
+
+    auto *s = new rt_scene();
+    s->device = device;
+    s->time0 = d->time0;
+    s->time1 = d->time1;
+    auto cleanup = [&](int rc) { rt_scene_destroy(s); return rc; };
+
+    std::vector<rt_dprim> prims(d->nprims), bprims(d->nboundary);
+    for (int i = 0; i < d->nprims; i++) {
+        const int src = bvh.order[i];
+        prims[i] = to_dprim(d->prims[src], src);
+        s->has_moving |= d->prims[src].kind == RT_PRIM_MOVING_SPHERE;
+    }
+    for (int i = 0; i < d->nboundary; i++) {
+        bprims[i] = to_dprim(d->boundary_prims[i], i);
+        s->has_moving |= d->boundary_prims[i].kind == RT_PRIM_MOVING_SPHERE;
+    }
+    std::vector<rt_dmaterial> mats(d->nmaterials);
+    for (int i = 0; i < d->nmaterials; i++) {
+        const rt_material &m = d->materials[i];
+        rt_dmaterial &o = mats[i];
+        o.kind = m.kind;
+        o.texture = m.texture;
+        o.fuzz = m.fuzz;
+        o.ref_idx = m.ref_idx;
+        for (int k = 0; k < 3; k++) o.albedo[k] = m.albedo[k];
+        o.flags = 0;
+    }
+    std::vector<rt_dtexture> texs(d->ntextures);
+    for (int i = 0; i < d->ntextures; i++) {
+        const rt_texture &t = d->textures[i];
+        rt_dtexture &o = texs[i];
+        o.kind = t.kind;
+        o.even = t.even;
+        o.odd = t.odd;
+        o.scale = t.scale;
+        for (int k = 0; k < 3; k++) o.color[k] = t.color[k];
+    }
+    std::vector<rt_dinstance> insts(d->ninstances);
+    for (int i = 0; i < d->ninstances; i++) {
+        const rt_instance &in = d->instances[i];
+        rt_dinstance &o = insts[i];
+        o.nops = in.nops;
+        for (int k = 0; k < in.nops; k++) {
+            o.ops[k][0] = fbits((int)in.ops[k][0]);   // op code as integer bits
+            for (int c = 1; c < 4; c++) o.ops[k][c] = in.ops[k][c];
+        }
+    }
+    std::vector<rt_dmedium> media(d->nmedia);
+    for (int i = 0; i < d->nmedia; i++) {
+        media[i].first = d->media[i].boundary_first;
+        media[i].count = d->media[i].boundary_count;
+        media[i].density = d->media[i].density;
+        media[i].material = d->media[i].material;
+    }
+    std::vector<float> ranvec(256 * 4, 0.0f);
+    for (int i = 0; i < 256; i++) for (int k = 0; k < 3; k++) ranvec[4 * i + k] = d->perlin_ranvec[3 * i + k];
+    std::vector<int32_t> perm(d->perlin_perm, d->perlin_perm + 768);
+    for (int v : perm) if (v < 0 || v > 255) return cleanup(fail(RT_ERR_INVALID, "Perlin permutation entry out of range"));
+
+    int rc;
+    if ((rc = upload(&s->nodes, bvh.nodes)) || (rc = upload(&s->prims, prims)) || (rc = upload(&s->bprims, bprims)) ||
+        (rc = upload(&s->media, media)) || (rc = upload(&s->mats, mats)) || (rc = upload(&s->texs, texs)) ||
+        (rc = upload(&s->insts, insts)) || (rc = upload(&s->ranvec, ranvec)) || (rc = upload(&s->perm, perm)))
+        return cleanup(rc);
+    s->root = bvh.root;
+    s->has_bvh = d->nprims > 0;
+    s->nmedia = d->nmedia;
+    s->bvh_depth = bvh.depth;
+    s->nnodes = (int)bvh.nodes.size();
+    s->nprims = d->nprims;
+
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return cleanup(hip_fail(e, "hipGetDeviceProperties"));
+    s->cus = prop.multiProcessorCount;
+    int bpc = 0, bpc_count = 0;
+    if ((e = rt_megakernel_occupancy(&bpc, false)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+    if ((e = rt_megakernel_occupancy(&bpc_count, true)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+    s->grid = std::max(1, bpc) * s->cus;
+    s->grid_count = std::max(1, bpc_count) * s->cus;
+    if ((e = hipMalloc(&s->counter, 64)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc counter"));
+    if ((e = hipMalloc(&s->stats, RT_CNT_N * sizeof(unsigned long long))) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc stats"));
+    for (auto &ev : s->ev)
+        if ((e = hipEventCreate(&ev)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
+    if ((e = hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking)) != hipSuccess)
+        return cleanup(hip_fail(e, "hipStreamCreate"));
+    *out = s;
+    return RT_OK;
+}
+
+// Job pixel order: tiles in the order given; inside a tile, 8x8 pixel blocks so
+// that the 64 lanes of a wave start on neighbouring pixels (coherent primary rays).
+static int prepare_job(rt_scene *s, const int32_t *tiles, int ntiles, int nx, int ny) {
+    std::vector<int32_t> key(tiles, tiles + 4 * ntiles);
+    if (key == s->job_tiles && s->job_xy) return RT_OK;
+    std::vector<uint32_t> xy, oi;
+    uint32_t base = 0;
+    for (int t = 0; t < ntiles; t++) {
+        const int x0 = tiles[4 * t], y0 = tiles[4 * t + 1], w = tiles[4 * t + 2], h = tiles[4 * t + 3];
+        if (w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > nx || y0 + h > ny || nx > 65535 || ny > 65535)
+            return fail(RT_ERR_INVALID, "tile outside the image");
+        for (int by = 0; by < h; by += 8)
+            for (int bx = 0; bx < w; bx += 8)
+                for (int yy = by; yy < std::min(by + 8, h); yy++)
+                    for (int xx = bx; xx < std::min(bx + 8, w); xx++) {
+                        xy.push_back((uint32_t)(x0 + xx) | ((uint32_t)(y0 + yy) << 16));
+                        oi.push_back(base + (uint32_t)(yy * w + xx));
+                    }
+        base += (uint32_t)(w * h);
+    }
+    if (s->job_xy) { (void)hipFree(s->job_xy); s->job_xy = nullptr; }
+    if (s->job_out) { (void)hipFree(s->job_out); s->job_out = nullptr; }
+    s->job_tiles.clear();
+    if (int rc = upload(&s->job_xy, xy)) return rc;
+    if (int rc = upload(&s->job_out, oi)) return rc;
+    s->npix = (uint32_t)xy.size();
+    s->job_tiles = key;
+    return RT_OK;
+}
+
+int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p, const int32_t *tiles, int ntiles,
+                    float *out_dev, void *stream_v, rt_stats *stats) {
+    if (!s || !cam || !p || !tiles || ntiles <= 0 || !out_dev) return fail(RT_ERR_INVALID, "rt_render_tiles: bad argument");
+    if (p->nx <= 0 || p->ny <= 0 || p->spp <= 0 || p->max_depth < 0) return fail(RT_ERR_INVALID, "bad render parameters");
+    if (s->has_moving && (cam->time0 < s->time0 || cam->time1 > s->time1))
+        return fail(RT_ERR_INVALID, "camera shutter outside the scene's time span (moving-sphere bounds)");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t stream = (hipStream_t)stream_v;
+    if (int rc = prepare_job(s, tiles, ntiles, p->nx, p->ny)) return rc;
+
+    const int chunk = p->chunk > 0 ? p->chunk : 16;
+    const int nchunks = (p->spp + chunk - 1) / chunk;
+    const uint64_t nitems = (uint64_t)s->npix * (uint64_t)nchunks;
+    if (nitems + 64 >= 0xFFFFFFFFull) return fail(RT_ERR_INVALID, "job too large for one launch (pixels x chunks >= 2^32)");
+    const size_t slab_bytes = (size_t)nitems * 16;
+    if (slab_bytes > s->slab_bytes) {
+        if (s->slab) (void)hipFree(s->slab);
+        s->slab = nullptr;
+        s->slab_bytes = 0;
+        HIP_TRY(hipMalloc(&s->slab, slab_bytes));
+        s->slab_bytes = slab_bytes;
+    }
+    const bool count = (p->flags & RT_FLAG_COUNT) != 0;
+    HIP_TRY(hipMemsetAsync(s->counter, 0, 64, stream));
+    if (count) HIP_TRY(hipMemsetAsync(s->stats, 0, RT_CNT_N * sizeof(unsigned long long), stream));
+
+    RtKernelArgs a{};
+    a.nodes = (const float4 *)s->nodes;
+    a.prims = (const float4 *)s->prims;
+    a.bprims = (const float4 *)s->bprims;
+    a.media = (const int4 *)s->media;
+    a.mats = (const float4 *)s->mats;
+    a.texs = (const float4 *)s->texs;
+    a.insts = (const float4 *)s->insts;
+    a.ranvec = (const float4 *)s->ranvec;
+    a.perm = (const int *)s->perm;
+    a.root = s->root;
+    a.has_bvh = s->has_bvh;
+    a.nmedia = s->nmedia;
+    for (int k = 0; k < 3; k++) {
+        a.org[k] = cam->origin[k];
+        a.llc[k] = cam->lower_left_corner[k];
+        a.hor[k] = cam->horizontal[k];
+        a.ver[k] = cam->vertical[k];
+        a.cu[k] = cam->u[k];
+        a.cv[k] = cam->v[k];
+    }
+    a.lens = cam->lens_radius;
+    a.ct0 = cam->time0;
+    a.ct1 = cam->time1;
+    a.nx = p->nx;
+    a.ny = p->ny;
+    a.ns = p->spp;
+    a.max_depth = p->max_depth;
+    a.tmin = p->t_min;
+    a.background = p->background;
+    a.chunk = chunk;
+    a.nchunks = nchunks;
+    a.sample_offset = p->sample_offset;
+    a.seed = p->seed;
+    a.job_xy = (const uint32_t *)s->job_xy;
+    a.npix = s->npix;
+    a.nitems = (uint32_t)nitems;
+    a.slab = (float4 *)s->slab;
+    a.counter = (uint32_t *)s->counter;
+    a.stats = (unsigned long long *)s->stats;
+
+    const float k = (float)(1.0 / (double)(float)p->spp);   // vec3::operator/= (vec3.h:134-141)
+    HIP_TRY(hipEventRecord(s->ev[0], stream));
+    HIP_TRY(rt_launch_megakernel(&a, count ? s->grid_count : s->grid, count, stream));
+    HIP_TRY(hipEventRecord(s->ev[1], stream));
+    HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, nchunks, k, (const uint32_t *)s->job_out, out_dev, stream));
+    HIP_TRY(hipEventRecord(s->ev[2], stream));
+
+    if (stats) {
+        HIP_TRY(hipEventSynchronize(s->ev[2]));
+        float ms0 = 0, ms1 = 0;
+        HIP_TRY(hipEventElapsedTime(&ms0, s->ev[0], s->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&ms1, s->ev[1], s->ev[2]));
+        std::memset(stats, 0, sizeof *stats);
+        stats->samples = (double)s->npix * (double)p->spp;
+        stats->kernel_ms = ms0;
+        stats->resolve_ms = ms1;
+        if (count) {
+            unsigned long long c[RT_CNT_N];
+            HIP_TRY(hipMemcpy(c, s->stats, sizeof c, hipMemcpyDeviceToHost));
+            stats->samples = (double)c[RT_CNT_SAMPLES];
+            stats->segments = (double)c[RT_CNT_SEGMENTS];
+            stats->node_visits = (double)c[RT_CNT_NODES];
+            stats->prim_tests = (double)c[RT_CNT_PRIMS];
+            stats->medium_tests = (double)c[RT_CNT_MEDIA];
+            stats->noise_evals = (double)c[RT_CNT_NOISE];
+            // SURVEY §8d byte model: 64 B per node fetch, 64 B per primitive record
+            // tested, per medium evaluation two boundary passes over its records
+            // (counted at 2 x 64 B), per segment the 32 B material record plus up to
+            // 32 B of texture record, per noise evaluation 7 octaves x 8 gradient
+            // gathers x (16 B gradient + 3 x 4 B permutation), and 16 B per work
+            // item of partial-sum slab traffic written + read back.
+            stats->algorithmic_bytes = 64.0 * stats->node_visits + 64.0 * stats->prim_tests +
+                                       128.0 * stats->medium_tests + 64.0 * stats->segments +
+                                       7.0 * 8.0 * 28.0 * stats->noise_evals + 32.0 * (double)nitems;
+        }
+    }
+    return RT_OK;
+}
+
+int rt_render_tile(rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p, int x0, int y0, int w, int h,
+                   float *out_rgb, rt_stats *stats) {
+    if (!s || !out_rgb) return fail(RT_ERR_INVALID, "rt_render_tile: bad argument");
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+    if (w <= 0 || h <= 0) return fail(RT_ERR_INVALID, "empty tile");
+    if (bytes > s->host_out_bytes) {
+        if (s->host_out) (void)hipFree(s->host_out);
+        s->host_out = nullptr;
+        s->host_out_bytes = 0;
+        HIP_TRY(hipMalloc(&s->host_out, bytes));
+        s->host_out_bytes = bytes;
+    }
+    const int32_t tile[4] = {x0, y0, w, h};
+    rt_stats local;
+    if (int rc = rt_render_tiles(s, cam, p, tile, 1, (float *)s->host_out, s->own_stream, stats ? stats : &local)) return rc;
+    HIP_TRY(hipMemcpyAsync(out_rgb, s->host_out, bytes, hipMemcpyDeviceToHost, s->own_stream));
+    HIP_TRY(hipStreamSynchronize(s->own_stream));
+    return RT_OK;
+}
+
+// ---------------------------------------------------------------- resolve
+void rt_quantize(const float *mean, int64_t n, uint8_t *rgb) {   // main.cpp:316-325
+    for (int64_t q = 0; q < n; q++) {
+        for (int k = 0; k < 3; k++) {
+            const float c = std::sqrt(mean[3 * q + k]);
+            int iv = int(255.99 * c);
+            iv = iv > 255 ? 255 : iv;
+            rgb[3 * q + k] = (uint8_t)iv;
+        }
+    }
+}
+
+int64_t rt_ppm_text(const uint8_t *rgb, int nx, int ny, char *buf, int64_t cap) {   // main.cpp:297, 327-330
+    std::string s = "P3\n" + std::to_string(nx) + " " + std::to_string(ny) + "\n255\n";
+    for (int64_t q = 0; q < (int64_t)nx * ny; q++)
+        s += std::to_string(rgb[3 * q]) + " " + std::to_string(rgb[3 * q + 1]) + " " + std::to_string(rgb[3 * q + 2]) + "\n";
+    if (buf && cap >= (int64_t)s.size()) std::memcpy(buf, s.data(), s.size());
+    return (int64_t)s.size();
+}
+
+// ------------------------------------------------------- host scene building
+static std::mutex g_desc_mu;
+static std::map<const rt_scene_desc *, std::unique_ptr<rtnw::flat_scene>> g_descs;
+
+int rt_builtin_scene_desc(const char *name, rt_scene_desc **out) {
+    if (!name || !out) return fail(RT_ERR_INVALID, "rt_builtin_scene_desc: null argument");
+    std::lock_guard<std::mutex> lk(g_desc_mu);
+    float t0, t1;
+    rtnw::hitable *world = rtnw::build_named_scene(name, &t0, &t1);
+    if (!world) return fail(RT_ERR_INVALID, std::string("unknown scene: ") + name);
+    std::unique_ptr<rtnw::flat_scene> fs;
+    try {
+        fs = rtnw::flatten_world(world, t0, t1);
+    } catch (const std::exception &ex) {
+        return fail(RT_ERR_UNSUPPORTED, ex.what());
+    }
+    *out = &fs->desc;
+    g_descs[&fs->desc] = std::move(fs);
+    return RT_OK;
+}
+
+void rt_scene_desc_free(rt_scene_desc *d) {
+    std::lock_guard<std::mutex> lk(g_desc_mu);
+    g_descs.erase(d);
+}
+
+int64_t rt_scene_desc_dump(const rt_scene_desc *d, char *buf, int64_t cap) {
+    if (!d) return fail(RT_ERR_INVALID, "null descriptor");
+    const std::string s = rtnw::dump_desc(d);
+    if (buf && cap >= (int64_t)s.size()) std::memcpy(buf, s.data(), s.size());
+    return (int64_t)s.size();
+}
+
+}  // extern "C"

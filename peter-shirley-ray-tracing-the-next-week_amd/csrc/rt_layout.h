@@ -1,0 +1,81 @@
+// rt_layout.h — the scene's layout in HBM, shared by the host uploader
+// (capi.cpp) and the megakernel (rt_kernel.hip).
+//
+// Everything the traversal touches is a 16-byte-aligned record read with
+// dwordx4 loads: an incoherent wave fetches one whole record per lane per
+// cache line instead of gathering scattered scalars.  Records are grouped by
+// role (nodes / primitives / boundary primitives / materials / textures /
+// instances / Perlin tables) in separate arrays.
+#pragma once
+#include <stdint.h>
+
+#include "rt_hip.h"   // enum values (prim / material / texture kinds, ops)
+
+#define RT_STACK_DEPTH 32          // traversal stack entries per lane (LDS)
+#define RT_MAX_BVH_DEPTH 31        // builder guarantee: a root-to-leaf path has <= 31 internal nodes
+#define RT_MAX_LEAF 8              // primitives per leaf
+#define RT_MAX_INSTANCE_OPS 6
+#define RT_MAX_CHECKER_DEPTH 16
+
+// Child reference in a node: bit 31 set = leaf, bits 24..30 = count-1, bits 0..23 = first prim.
+#define RT_LEAF_BIT 0x80000000u
+#define RT_EMPTY_CHILD 0xFFFFFFFFu
+#define RT_LEAF_REF(first, count) (RT_LEAF_BIT | ((uint32_t)((count) - 1) << 24) | (uint32_t)(first))
+#define RT_LEAF_FIRST(ref) ((ref) & 0x00FFFFFFu)
+#define RT_LEAF_COUNT(ref) ((((ref) >> 24) & 0x7Fu) + 1)
+
+// BVH2 node, 64 B: the boxes of BOTH children, so one node fetch decides which
+// children to enter.  b0..b2 hold the boxes as
+//   b0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+//   b1 = (c0.lo.z, c0.hi.z, c1.lo.x, c1.hi.x)
+//   b2 = (c1.lo.y, c1.hi.y, c1.lo.z, c1.hi.z)
+//   ch = (child0, child1, -, -)
+struct rt_dnode {
+    float b0[4], b1[4], b2[4];
+    uint32_t ch[4];
+};
+
+// Primitive, 64 B.  g0..g2 by kind:
+//   sphere:        g0 = (cx, cy, cz, r)
+//   moving sphere: g0 = (c0x, c0y, c0z, r), g1 = (c1x-c0x, c1y-c0y, c1z-c0z, t0), g2 = (t1-t0, ...)
+//   rects:         g0 = (a0, a1, b0, b1), g1 = (k, ...)
+// m = (kind | flip << 8, material, instance (-1 none), list order)
+struct rt_dprim {
+    float g0[4], g1[4], g2[4];
+    int32_t m[4];
+};
+
+// Material, 32 B: (kind, texture, fuzz, ref_idx) + (albedo.xyz, flags)
+struct rt_dmaterial {
+    int32_t kind, texture;
+    float fuzz, ref_idx;
+    float albedo[3];
+    int32_t flags;
+};
+
+// Texture, 32 B: (kind, even, odd, scale) + (color.xyz, -)
+struct rt_dtexture {
+    int32_t kind, even, odd;
+    float scale;
+    float color[3];
+    int32_t pad;
+};
+
+// Instance transform chain, 112 B: (nops, -, -, -) + 6 x (op, a, b, c), outermost first.
+struct rt_dinstance {
+    int32_t nops, pad[3];
+    float ops[RT_MAX_INSTANCE_OPS][4];
+};
+
+// Medium, 16 B: (boundary_first, boundary_count, density, phase material)
+struct rt_dmedium {
+    int32_t first, count;
+    float density;
+    int32_t material;
+};
+
+// Counters of the RT_FLAG_COUNT kernel variant (uint64 each).
+enum {
+    RT_CNT_SAMPLES = 0, RT_CNT_SEGMENTS, RT_CNT_NODES, RT_CNT_PRIMS, RT_CNT_MEDIA, RT_CNT_NOISE,
+    RT_CNT_SHADES, RT_CNT_INSTANCED, RT_CNT_N
+};

@@ -1,0 +1,303 @@
+"""rtnw.py — Python view of librt_hip.so (include/rt_hip.h) via ctypes.
+
+The path tracer's product is the C ABI; this module is the host-side mirror the
+tests and bench.py drive it through, named after the reference's interface:
+
+    scene  = Scene.builtin("final")             # main.cpp:190-230 built by the host API
+    cam    = Camera.preset("cornell", nx, ny)   # camera.h:21-39 (main.cpp:254-259)
+    mean   = scene.render_tile(cam, RenderParams(nx=.., ny=.., spp=..), 0, 0, nx, ny)
+    ppm    = ppm_text(quantize(mean))           # main.cpp:314-330
+
+There is no CPU fallback: every render goes through the HIP megakernel, and
+loading fails loudly when librt_hip.so is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librt_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "rt_hip.h")
+
+RT_OK = 0
+RT_BG_BLACK, RT_BG_SKY = 0, 1
+RT_FLAG_COUNT = 1
+
+
+class RtError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"rt_hip error {code}: {msg}")
+        self.code = code
+
+
+class RtPrim(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("material", ctypes.c_int32), ("instance", ctypes.c_int32),
+                ("flip", ctypes.c_int32), ("p", ctypes.c_float * 12)]
+
+
+class RtInstance(ctypes.Structure):
+    _fields_ = [("nops", ctypes.c_int32), ("pad", ctypes.c_int32 * 3), ("ops", (ctypes.c_float * 4) * 6)]
+
+
+class RtMaterial(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("texture", ctypes.c_int32), ("fuzz", ctypes.c_float),
+                ("ref_idx", ctypes.c_float), ("albedo", ctypes.c_float * 3), ("pad", ctypes.c_int32)]
+
+
+class RtTexture(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("even", ctypes.c_int32), ("odd", ctypes.c_int32),
+                ("scale", ctypes.c_float), ("color", ctypes.c_float * 3), ("image", ctypes.c_int32)]
+
+
+class RtMedium(ctypes.Structure):
+    _fields_ = [("boundary_first", ctypes.c_int32), ("boundary_count", ctypes.c_int32), ("density", ctypes.c_float),
+                ("material", ctypes.c_int32), ("order", ctypes.c_int32), ("pad", ctypes.c_int32 * 3)]
+
+
+class RtSceneDesc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_uint32), ("nprims", ctypes.c_int32), ("nboundary", ctypes.c_int32),
+                ("nmedia", ctypes.c_int32), ("nmaterials", ctypes.c_int32), ("ntextures", ctypes.c_int32),
+                ("ninstances", ctypes.c_int32),
+                ("prims", ctypes.POINTER(RtPrim)), ("boundary_prims", ctypes.POINTER(RtPrim)),
+                ("media", ctypes.POINTER(RtMedium)), ("materials", ctypes.POINTER(RtMaterial)),
+                ("textures", ctypes.POINTER(RtTexture)), ("instances", ctypes.POINTER(RtInstance)),
+                ("perlin_ranvec", ctypes.POINTER(ctypes.c_float)), ("perlin_perm", ctypes.POINTER(ctypes.c_int32)),
+                ("time0", ctypes.c_float), ("time1", ctypes.c_float)]
+
+
+class RtCameraDesc(ctypes.Structure):
+    _fields_ = [("origin", ctypes.c_float * 3), ("lower_left_corner", ctypes.c_float * 3),
+                ("horizontal", ctypes.c_float * 3), ("vertical", ctypes.c_float * 3), ("u", ctypes.c_float * 3),
+                ("v", ctypes.c_float * 3), ("w", ctypes.c_float * 3), ("lens_radius", ctypes.c_float),
+                ("time0", ctypes.c_float), ("time1", ctypes.c_float)]
+
+
+class RtRenderParams(ctypes.Structure):
+    _fields_ = [("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("spp", ctypes.c_int32), ("max_depth", ctypes.c_int32),
+                ("t_min", ctypes.c_float), ("background", ctypes.c_int32), ("chunk", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("sample_offset", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+                ("seed", ctypes.c_uint64)]
+
+
+class RtStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ("samples", "segments", "node_visits", "prim_tests", "medium_tests",
+                                               "noise_evals", "algorithmic_bytes", "kernel_ms", "resolve_ms")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Loads librt_hip.so (torch first, so one HIP runtime serves both)."""
+    global _lib
+    if _lib is None:
+        try:  # if torch is present, bind its HIP runtime (same SONAME) before ours
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {HERE}` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        sig = {
+            "rt_camera_init": (ctypes.c_int, [P(RtCameraDesc), P(ctypes.c_float), P(ctypes.c_float), P(ctypes.c_float),
+                                              ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                              ctypes.c_float, ctypes.c_float]),
+            "rt_scene_create": (ctypes.c_int, [P(RtSceneDesc), ctypes.c_int, P(ctypes.c_void_p)]),
+            "rt_scene_destroy": (None, [ctypes.c_void_p]),
+            "rt_render_tile": (ctypes.c_int, [ctypes.c_void_p, P(RtCameraDesc), P(RtRenderParams), ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, P(RtStats)]),
+            "rt_render_tiles": (ctypes.c_int, [ctypes.c_void_p, P(RtCameraDesc), P(RtRenderParams), ctypes.c_void_p,
+                                               ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, P(RtStats)]),
+            "rt_device_alloc": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, P(ctypes.c_void_p)]),
+            "rt_device_free": (ctypes.c_int, [ctypes.c_void_p]),
+            "rt_copy_to_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+            "rt_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+            "rt_quantize": (None, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+            "rt_ppm_text": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int64]),
+            "rt_builtin_scene_desc": (ctypes.c_int, [ctypes.c_char_p, P(P(RtSceneDesc))]),
+            "rt_scene_desc_free": (None, [P(RtSceneDesc)]),
+            "rt_scene_desc_dump": (ctypes.c_int64, [P(RtSceneDesc), ctypes.c_char_p, ctypes.c_int64]),
+            "rt_last_error": (ctypes.c_char_p, []),
+            "rt_version": (ctypes.c_char_p, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != RT_OK:
+        raise RtError(rc, lib().rt_last_error().decode())
+    return rc
+
+
+def header_symbols(path: str = HEADER):
+    """Function names declared in include/rt_hip.h."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(rt_\w+)\s*\(", text, flags=re.M)))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().rt_device_count(ctypes.byref(n))
+    return n.value if rc == RT_OK else 0
+
+
+# --------------------------------------------------------------------- camera
+CAMERA_PRESETS = {   # main.cpp:254-276
+    "cornell": dict(lookfrom=(228, 278, -800), lookat=(278, 278, 0), vfov=40.0, aperture=0.0),
+    "random": dict(lookfrom=(13, 2, 3), lookat=(0, 0, 0), vfov=20.0, aperture=0.1),
+    "final_alt": dict(lookfrom=(478, 278, -600), lookat=(278, 278, 0), vfov=20.0, aperture=0.0),
+}
+
+
+class Camera:
+    def __init__(self, lookfrom, lookat, vup, vfov, aspect, aperture, focus_dist, t0=0.0, t1=1.0):
+        f3 = ctypes.c_float * 3
+        self.desc = RtCameraDesc()
+        _check(lib().rt_camera_init(ctypes.byref(self.desc), f3(*lookfrom), f3(*lookat), f3(*vup), vfov, aspect,
+                                    aperture, focus_dist, t0, t1))
+
+    @classmethod
+    def preset(cls, name, nx, ny):
+        p = CAMERA_PRESETS[name]
+        aspect = float(np.float32(nx) / np.float32(ny))
+        return cls(p["lookfrom"], p["lookat"], (0, 1, 0), p["vfov"], aspect, p["aperture"], 10.0, 0.0, 1.0)
+
+    def as_array(self):
+        d = self.desc
+        return np.array(list(d.origin) + list(d.lower_left_corner) + list(d.horizontal) + list(d.vertical) +
+                        list(d.u) + list(d.v) + list(d.w) + [d.lens_radius, d.time0, d.time1], dtype=np.float32)
+
+
+# ---------------------------------------------------------------------- scene
+SCENE_DEFAULTS = {   # per-scene camera / background / depth pairing
+    "random_scene": ("random", RT_BG_SKY, 8),
+    "random_motion": ("random", RT_BG_SKY, 50),
+    "cornell_box": ("cornell", RT_BG_BLACK, 50),
+    "cornell_smoke": ("cornell", RT_BG_BLACK, 50),
+    "final": ("cornell", RT_BG_BLACK, 50),
+    "simple_light": ("random", RT_BG_BLACK, 50),
+    "two_spheres": ("random", RT_BG_BLACK, 50),
+    "test": ("random", RT_BG_BLACK, 50),
+}
+
+
+def RenderParams(nx, ny, spp, max_depth=50, t_min=0.001, background=RT_BG_BLACK, chunk=0, flags=0, seed=0,
+                 sample_offset=0) -> RtRenderParams:
+    return RtRenderParams(nx=nx, ny=ny, spp=spp, max_depth=max_depth, t_min=t_min, background=background,
+                          chunk=chunk, flags=flags, sample_offset=sample_offset, seed=seed)
+
+
+class SceneDesc:
+    """A flattened scene built by the host API (owned by librt_hip)."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    @classmethod
+    def builtin(cls, name: str) -> "SceneDesc":
+        p = ctypes.POINTER(RtSceneDesc)()
+        _check(lib().rt_builtin_scene_desc(name.encode(), ctypes.byref(p)))
+        return cls(p)
+
+    def dump(self) -> str:
+        n = lib().rt_scene_desc_dump(self.ptr, None, 0)
+        buf = ctypes.create_string_buffer(int(n))
+        lib().rt_scene_desc_dump(self.ptr, buf, n)
+        return buf.raw[:n].decode()
+
+    @property
+    def contents(self) -> RtSceneDesc:
+        return self.ptr.contents
+
+    def free(self):
+        if self.ptr:
+            lib().rt_scene_desc_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Scene:
+    """A scene resident in one GPU's HBM (rt_scene_create)."""
+
+    def __init__(self, desc: SceneDesc, device: int = 0):
+        self.desc = desc
+        self.handle = ctypes.c_void_p()
+        _check(lib().rt_scene_create(desc.ptr, device, ctypes.byref(self.handle)))
+
+    @classmethod
+    def builtin(cls, name: str, device: int = 0) -> "Scene":
+        return cls(SceneDesc.builtin(name), device)
+
+    def render_tile(self, cam: Camera, params: RtRenderParams, x0, y0, w, h, stats: bool = False):
+        out = np.zeros((h, w, 3), dtype=np.float32)
+        st = RtStats()
+        _check(lib().rt_render_tile(self.handle, ctypes.byref(cam.desc), ctypes.byref(params), x0, y0, w, h,
+                                    out.ctypes.data, ctypes.byref(st)))
+        return (out, st.as_dict()) if stats else out
+
+    def render_tiles(self, cam: Camera, params: RtRenderParams, tiles, out_dev_ptr: int, stream_ptr: int = 0,
+                     stats: bool = True):
+        t = np.ascontiguousarray(np.asarray(tiles, dtype=np.int32).reshape(-1, 4))
+        st = RtStats()
+        _check(lib().rt_render_tiles(self.handle, ctypes.byref(cam.desc), ctypes.byref(params), t.ctypes.data,
+                                     int(t.shape[0]), ctypes.c_void_p(out_dev_ptr), ctypes.c_void_p(stream_ptr),
+                                     ctypes.byref(st) if stats else None))
+        return st.as_dict()
+
+    def close(self):
+        if self.handle:
+            lib().rt_scene_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# -------------------------------------------------------------------- resolve
+def quantize(mean: np.ndarray) -> np.ndarray:
+    m = np.ascontiguousarray(mean, dtype=np.float32)
+    out = np.zeros(m.shape, dtype=np.uint8)
+    lib().rt_quantize(m.ctypes.data, m.size // 3, out.ctypes.data)
+    return out
+
+
+def ppm_text(rgb: np.ndarray) -> bytes:
+    r = np.ascontiguousarray(rgb, dtype=np.uint8)
+    h, w, _ = r.shape
+    n = lib().rt_ppm_text(r.ctypes.data, w, h, None, 0)
+    buf = ctypes.create_string_buffer(int(n))
+    lib().rt_ppm_text(r.ctypes.data, w, h, buf, n)
+    return buf.raw[:n]
+
+
+def tiles_for_rank(nx, ny, tile, rank, world):
+    """Interleaved tile assignment: tile k (row-major over the image) goes to rank k % world."""
+    out = []
+    k = 0
+    for y0 in range(0, ny, tile):
+        for x0 in range(0, nx, tile):
+            if k % world == rank:
+                out.append((x0, y0, min(tile, nx - x0), min(tile, ny - y0)))
+            k += 1
+    return out

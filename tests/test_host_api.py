@@ -1,0 +1,137 @@
+"""Host side of the product (librt_hip.so), no GPU needed.
+
+* the library loads and exports every function include/rt_hip.h declares;
+* the host API's scene builders + flattener reproduce the reference's scenes
+  exactly (leaf dump == reference dump, golden SHA-256);
+* the camera, quantiser and PPM writer match the reference arithmetic;
+* without a GPU, rendering fails loudly (there is no CPU fallback).
+"""
+import ctypes
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+import rtnw
+
+
+def test_library_exports_every_header_symbol():
+    L = rtnw.lib()
+    declared = rtnw.header_symbols()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", rtnw.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert set(declared) <= exported
+
+
+def test_library_has_gfx950_code_object():
+    # the offload bundle carries the target triple amdgcn-amd-amdhsa--gfx950
+    data = open(rtnw.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+@pytest.mark.parametrize("scene", list(O.SCENES))
+def test_scene_builders_match_reference(golden, scene):
+    d = rtnw.SceneDesc.builtin(scene)
+    text = d.dump()
+    assert hashlib.sha256(text.encode()).hexdigest() == golden["scene_dump_sha256"][scene]
+    assert text == O.scene_dump(scene)
+
+
+def test_final_scene_shape():
+    keep = rtnw.SceneDesc.builtin("final")   # owns the arrays .contents points into
+    d = keep.contents
+    # 100 boxes x 6 rects + light + moving sphere + 3 spheres + noise sphere + 1000 spheres
+    assert d.nprims == 600 + 1 + 1 + 3 + 1 + 1000
+    assert d.nmedia == 2 and d.nboundary == 2
+    kinds = [d.prims[i].kind for i in range(d.nprims)]
+    assert kinds.count(1) == 1 and kinds.count(0) == 1004
+
+
+def test_cornell_instances():
+    keep = rtnw.SceneDesc.builtin("cornell_box")
+    d = keep.contents
+    assert d.ninstances == 2
+    ops = [[d.instances[i].ops[k][0] for k in range(d.instances[i].nops)] for i in range(2)]
+    assert ops == [[1.0, 2.0], [1.0, 2.0]]      # translate(rotate_y(box)), outermost first
+
+
+def _oracle_camera(preset, nx, ny):
+    """camera.h:21-39 restated in numpy float32 (the oracle keeps its camera private)."""
+    f = np.float32
+    p = rtnw.CAMERA_PRESETS[preset]
+    lookfrom = np.array(p["lookfrom"], f)
+    lookat = np.array(p["lookat"], f)
+    vup = np.array([0, 1, 0], f)
+    aspect = f(nx) / f(ny)
+    fd = f(10.0)
+
+    def unit(v):
+        return v / f(np.sqrt(f(f(v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])))
+
+    def cross(a, b):
+        return np.array([a[1] * b[2] - a[2] * b[1], -(a[0] * b[2] - a[2] * b[0]), a[0] * b[1] - a[1] * b[0]], f)
+    theta = f(np.float64(f(p["vfov"])) * np.pi / 180)
+    hh = f(np.tan(np.float32(theta / f(2))))
+    hw = f(aspect * hh)
+    w = unit(lookfrom - lookat)
+    u = unit(cross(vup, w))
+    v = cross(w, u)
+    llc = ((lookfrom - f(hw * fd) * u) - f(hh * fd) * v) - fd * w
+    return llc, f(f(f(2) * hw) * fd) * u, f(f(f(2) * hh) * fd) * v
+
+
+@pytest.mark.parametrize("preset,nx,ny", [("cornell", 500, 500), ("random", 200, 100), ("random", 800, 400)])
+def test_camera_matches_reference_arithmetic(preset, nx, ny):
+    cam = rtnw.Camera.preset(preset, nx, ny)
+    llc, hor, ver = _oracle_camera(preset, nx, ny)
+    d = cam.desc
+    assert np.allclose(np.array(d.lower_left_corner), llc, rtol=2e-7, atol=1e-6)
+    assert np.allclose(np.array(d.horizontal), hor, rtol=2e-7)
+    assert np.allclose(np.array(d.vertical), ver, rtol=2e-7)
+    assert d.lens_radius == np.float32(rtnw.CAMERA_PRESETS[preset]["aperture"]) / 2
+
+
+def test_quantize_and_ppm_match_oracle():
+    rng = np.random.default_rng(0)
+    mean = (rng.random((7, 9, 3)) * 1.5).astype(np.float32)
+    mean[0, 0] = [0.0, 1.0, 4.0]
+    a = rtnw.quantize(mean)
+    b = O.quantize(mean)
+    assert np.array_equal(a, b)
+    assert rtnw.ppm_text(a) == O.ppm_text(b)
+    assert a[0, 0].tolist() == [0, 255, 255]
+
+
+def test_tiles_cover_image_once():
+    nx, ny, t = 100, 70, 32
+    seen = np.zeros((ny, nx), np.int32)
+    for r in range(3):
+        for x0, y0, w, h in rtnw.tiles_for_rank(nx, ny, t, r, 3):
+            seen[y0:y0 + h, x0:x0 + w] += 1
+    assert (seen == 1).all()
+
+
+@pytest.mark.skipif(rtnw.device_count() > 0, reason="a GPU is present")
+def test_no_cpu_fallback_without_gpu():
+    with pytest.raises(rtnw.RtError) as e:
+        rtnw.Scene.builtin("cornell_box")
+    assert e.value.code == -2   # RT_ERR_HIP
+
+
+def test_descriptor_validation_rejects_bad_material():
+    d = rtnw.SceneDesc.builtin("two_spheres")
+    c = d.contents
+    saved = c.prims[0].material
+    c.prims[0].material = 999
+    try:
+        h = ctypes.c_void_p()
+        rc = rtnw.lib().rt_scene_create(d.ptr, 0, ctypes.byref(h))
+        assert rc == -1
+        assert b"material" in rtnw.lib().rt_last_error()
+    finally:
+        c.prims[0].material = saved

@@ -1,0 +1,32 @@
+#!/bin/bash
+# tools/gpu_session.sh STEP... — runs named GPU steps on the gpurun box, each under
+# its own time limit; logs go to gpurun_out/<step>.log.  A step that exits 0 or 1
+# (tests failed / assertion) lets the next step run; any other status (fault,
+# abort, segfault, timeout) ends the session there.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() {
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*" >> gpurun_out/steps.txt
+  local t0=$(date +%s)
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc $(( $(date +%s) - t0 ))s" | tee -a gpurun_out/steps.txt
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    build)  run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests)  run tests 1200 python -m pytest tests -m gpu -x -q -s ;;
+    testsk) run tests 1200 python -m pytest tests -m gpu -q -s ;;
+    bench_small) run bench_small 600 python bench.py --spp 64 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    bench)  run bench 900 python bench.py ;;
+    prof)   cd /tmp; export TMPDIR=/tmp; cd - >/dev/null
+            run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --spp 256 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
