@@ -202,7 +202,9 @@ def main():
                          "algorithmic_bytes_per_launch": alg,
                          "rays_per_sample": cst["segments"] / max(1.0, cst["samples"]),
                          "node_visits_per_ray": cst["node_visits"] / max(1.0, cst["segments"]),
-                         "prim_tests_per_ray": cst["prim_tests"] / max(1.0, cst["segments"])},
+                         "prim_tests_per_ray": (cst["sphere_tests"] + cst["moving_sphere_tests"] + cst["rect_tests"])
+                         / max(1.0, cst["segments"]),
+                         "algorithmic_bytes_per_sample": alg / max(1.0, cst["samples"])},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

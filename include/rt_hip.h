@@ -149,12 +149,16 @@ typedef struct rt_render_params {
 
 typedef struct rt_stats {
     double samples;               /* camera samples rendered */
-    double segments;              /* rays traced (RT_FLAG_COUNT) */
-    double node_visits;           /* BVH nodes fetched (RT_FLAG_COUNT) */
-    double prim_tests;            /* primitive intersection tests (RT_FLAG_COUNT) */
+    double segments;              /* rays traced = world hit calls (RT_FLAG_COUNT) */
+    double node_visits;           /* BVH2 nodes fetched, each holding both child boxes (RT_FLAG_COUNT) */
+    double sphere_tests;          /* sphere tests, BVH leaves + media boundaries (RT_FLAG_COUNT) */
+    double moving_sphere_tests;   /* (RT_FLAG_COUNT) */
+    double rect_tests;            /* xy/xz/yz rect tests (RT_FLAG_COUNT) */
+    double instanced_tests;       /* tests through a translate/rotate_y chain (RT_FLAG_COUNT) */
     double medium_tests;          /* constant_medium evaluations (RT_FLAG_COUNT) */
+    double shades;                /* material evaluations (RT_FLAG_COUNT) */
     double noise_evals;           /* Perlin turbulence evaluations (RT_FLAG_COUNT) */
-    double algorithmic_bytes;     /* SURVEY §8d byte model for the launch (RT_FLAG_COUNT) */
+    double algorithmic_bytes;     /* SURVEY §8d byte model for the launch (RT_FLAG_COUNT; DESIGN.md §Roofline) */
     double kernel_ms;             /* megakernel time from HIP events on the render stream */
     double resolve_ms;            /* partial-sum resolve kernel time */
 } rt_stats;

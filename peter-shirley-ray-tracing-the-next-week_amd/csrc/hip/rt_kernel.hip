@@ -168,7 +168,7 @@ __device__ __forceinline__ float rect_t(int axis, float4 g0, float k, const Ray 
 __device__ __forceinline__ int rect_axis(int kind) { return 4 - kind; }
 
 __device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float tmin,
-                                        int &key) {
+                                        int &key, int &kind_out) {
     const float4 g0 = P[idx * 4 + 0];
     const float4 g1 = P[idx * 4 + 1];
     const float4 g2 = P[idx * 4 + 2];
@@ -176,6 +176,7 @@ __device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, ui
     int kind = fbits(mm.x) & 0xff;
     int inst = fbits(mm.z);
     int order = fbits(mm.w);
+    kind_out = kind | (inst >= 0 ? 0x100 : 0);
     Ray r = r0;
     if (inst >= 0) r = to_object(insts, inst, r0);
     float t;
@@ -223,12 +224,26 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
 }
 
 // Closest boundary hit of a constant_medium (its own small list), t > / >= tmin.
+struct Counters {
+    uint64_t samples = 0, segments = 0, nodes = 0, spheres = 0, mspheres = 0, rects = 0, instanced = 0, media = 0,
+             shades = 0, noise = 0;
+    __device__ __forceinline__ void prim(int kind) {
+        const int k = kind & 0xff;
+        if (k == RT_PRIM_SPHERE) spheres++;
+        else if (k == RT_PRIM_MOVING_SPHERE) mspheres++;
+        else rects++;
+        if (kind & 0x100) instanced++;
+    }
+};
+
+template <bool kCount>
 __device__ __forceinline__ float boundary_t(const float4 *B, const float4 *insts, int first, int count, const Ray &r,
-                                            float tmin) {
+                                            float tmin, Counters &cnt) {
     float best = RT_INF;
     for (int q = 0; q < count; ++q) {
-        int key;
-        float t = prim_t(B, insts, (uint32_t)(first + q), r, tmin, key);
+        int key, kind;
+        float t = prim_t(B, insts, (uint32_t)(first + q), r, tmin, key, kind);
+        if (kCount) cnt.prim(kind);
         if (t < best) best = t;
     }
     return best;
@@ -277,7 +292,7 @@ __device__ float perlin_turb(const float4 *ranvec, const int *perm, V3 p) {   //
 }
 
 template <bool kCount>
-__device__ V3 tex_value(const RtKernelArgs &A, int ti, V3 p, uint64_t &noise_cnt) {   // texture.h:16-59
+__device__ V3 tex_value(const RtKernelArgs &A, int ti, V3 p, Counters &cnt) {   // texture.h:16-59
     for (int guard = 0; guard < RT_MAX_CHECKER_DEPTH; ++guard) {
         const float4 t0 = A.texs[ti * 2 + 0];
         const float4 t1 = A.texs[ti * 2 + 1];
@@ -289,7 +304,7 @@ __device__ V3 tex_value(const RtKernelArgs &A, int ti, V3 p, uint64_t &noise_cnt
             continue;
         }
         // RT_TEX_NOISE
-        if (kCount) noise_cnt++;
+        if (kCount) cnt.noise++;
         float sc = t0.w;
         float s = 1 + sinf(sc * p.x + 5 * perlin_turb(A.ranvec, A.perm, scale(sc, p)));
         float h = 0.5f * 1;
@@ -339,7 +354,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
     Rng g; g.key = 0; g.n = 0;
     uint32_t px = 0, py = 0;
 
-    uint64_t c_samples = 0, c_segments = 0, c_nodes = 0, c_prims = 0, c_media = 0, c_noise = 0, c_inst = 0;
+    Counters cnt;
 
 
     for (;;) {
@@ -405,13 +420,13 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
             beta = mk(1, 1, 1);
             depth = 0;
             path = true;
-            if (kCount) c_samples++;
+            if (kCount) cnt.samples++;
         }
 
         if (!path) continue;   // finished lanes idle until the wave drains
 
         // ---- 3. closest surface hit: BVH2, stack in LDS ------------------------
-        if (kCount) c_segments++;
+        if (kCount) cnt.segments++;
         float best_t = RT_FLT_MAX;
         int best_key = 0x7FFFFFFF;
         uint32_t best_prim = 0xFFFFFFFFu;
@@ -422,7 +437,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
             int sp = 0;
             for (;;) {
                 if (!(node & RT_LEAF_BIT)) {
-                    if (kCount) c_nodes++;
+                    if (kCount) cnt.nodes++;
                     const float4 b0 = A.nodes[node * 4 + 0];
                     const float4 b1 = A.nodes[node * 4 + 1];
                     const float4 b2 = A.nodes[node * 4 + 2];
@@ -451,11 +466,11 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
                     if (h0) { node = c0; continue; }
                     if (h1) { node = c1; continue; }
                 } else {
-                    const uint32_t first = RT_LEAF_FIRST(node), cnt = RT_LEAF_COUNT(node);
-                    for (uint32_t q = 0; q < cnt; ++q) {
-                        int key;
-                        float t = prim_t(A.prims, A.insts, first + q, r, A.tmin, key);
-                        if (kCount) c_prims++;
+                    const uint32_t first = RT_LEAF_FIRST(node), nleaf = RT_LEAF_COUNT(node);
+                    for (uint32_t q = 0; q < nleaf; ++q) {
+                        int key, kind;
+                        float t = prim_t(A.prims, A.insts, first + q, r, A.tmin, key, kind);
+                        if (kCount) cnt.prim(kind);
                         if (t < best_t || (t == best_t && key < best_key)) {
                             best_t = t; best_key = key; best_prim = first + q;
                         }
@@ -472,11 +487,11 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
         Hit hr;
         if (have) hr = prim_record(A.prims, A.insts, best_prim, r, best_t);
         for (int k = 0; k < A.nmedia; ++k) {
-            if (kCount) c_media++;
+            if (kCount) cnt.media++;
             const int4 md = A.media[k];
-            float r1 = boundary_t(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX);
+            float r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
             if (r1 == RT_INF) continue;
-            float r2 = boundary_t(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001));
+            float r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
             if (r2 == RT_INF) continue;
             float tmax = have ? best_t : RT_FLT_MAX;
             if (r1 < A.tmin) r1 = A.tmin;
@@ -509,12 +524,13 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
                 L = mul(beta, mk(0, 0, 0));
             }
         } else {
+            if (kCount) cnt.shades++;
             const float4 m0 = A.mats[hr.mat * 2 + 0];
             const float4 m1 = A.mats[hr.mat * 2 + 1];
             const int kind = fbits(m0.x);
             const int tex = fbits(m0.y);
             V3 emitted = mk(0, 0, 0);
-            if (kind == RT_MAT_DIFFUSE_LIGHT) emitted = tex_value<kCount>(A, tex, hr.p, c_noise);
+            if (kind == RT_MAT_DIFFUSE_LIGHT) emitted = tex_value<kCount>(A, tex, hr.p, cnt);
             bool scattered = false;
             V3 att = mk(0, 0, 0);
             Ray ns;
@@ -522,7 +538,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
                 if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
                     V3 target = add(add(hr.p, hr.n), random_in_unit_sphere(g));
                     ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
-                    att = tex_value<kCount>(A, tex, hr.p, c_noise);
+                    att = tex_value<kCount>(A, tex, hr.p, cnt);
                     scattered = true;
                 } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
                     V3 reflected = reflect(unit(r.d), hr.n);
@@ -567,7 +583,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
                     scattered = true;
                 } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
                     ns.o = hr.p; ns.d = random_in_unit_sphere(g); ns.time = 0.0f;
-                    att = tex_value<kCount>(A, tex, hr.p, c_noise);
+                    att = tex_value<kCount>(A, tex, hr.p, cnt);
                     scattered = true;
                 }
             }
@@ -591,7 +607,8 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
     }
 
     if (kCount) {
-        uint64_t v[RT_CNT_N] = {c_samples, c_segments, c_nodes, c_prims, c_media, c_noise, 0, c_inst};
+        uint64_t v[RT_CNT_N] = {cnt.samples, cnt.segments, cnt.nodes, cnt.spheres, cnt.mspheres, cnt.rects,
+                                cnt.instanced, cnt.media, cnt.shades, cnt.noise};
         for (int k = 0; k < RT_CNT_N; ++k) {
             uint64_t x = v[k];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);

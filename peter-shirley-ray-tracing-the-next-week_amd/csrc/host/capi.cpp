@@ -73,6 +73,19 @@ rt_dprim to_dprim(const rt_prim &p, int order) {
     return d;
 }
 
+// SURVEY §8d byte model (bytes the algorithm must read or write, independent of
+// this implementation's record padding):
+//   BVH2 node fetch 64 B (two child boxes + refs); sphere 16 B; moving sphere 36 B;
+//   rect 24 B; instance chain entered 32 B; medium record 16 B; material +
+//   texture per shade 16 + 16 B; Perlin turbulence 7 octaves x 8 gradient gathers
+//   x (12 B gradient + 3 x 4 B permutation) = 1344 B; per work item the 16-B
+//   partial sum written and read back; 12 B of output per pixel.
+double algorithmic_bytes(const rt_stats &st, double items, double pixels) {
+    return 64.0 * st.node_visits + 16.0 * st.sphere_tests + 36.0 * st.moving_sphere_tests + 24.0 * st.rect_tests +
+           32.0 * st.instanced_tests + 16.0 * st.medium_tests + 32.0 * st.shades + 1344.0 * st.noise_evals +
+           32.0 * items + 12.0 * pixels;
+}
+
 }  // namespace
 
 struct rt_scene {
@@ -432,18 +445,14 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->samples = (double)c[RT_CNT_SAMPLES];
             stats->segments = (double)c[RT_CNT_SEGMENTS];
             stats->node_visits = (double)c[RT_CNT_NODES];
-            stats->prim_tests = (double)c[RT_CNT_PRIMS];
+            stats->sphere_tests = (double)c[RT_CNT_SPHERES];
+            stats->moving_sphere_tests = (double)c[RT_CNT_MSPHERES];
+            stats->rect_tests = (double)c[RT_CNT_RECTS];
+            stats->instanced_tests = (double)c[RT_CNT_INSTANCED];
             stats->medium_tests = (double)c[RT_CNT_MEDIA];
+            stats->shades = (double)c[RT_CNT_SHADES];
             stats->noise_evals = (double)c[RT_CNT_NOISE];
-            // SURVEY §8d byte model: 64 B per node fetch, 64 B per primitive record
-            // tested, per medium evaluation two boundary passes over its records
-            // (counted at 2 x 64 B), per segment the 32 B material record plus up to
-            // 32 B of texture record, per noise evaluation 7 octaves x 8 gradient
-            // gathers x (16 B gradient + 3 x 4 B permutation), and 16 B per work
-            // item of partial-sum slab traffic written + read back.
-            stats->algorithmic_bytes = 64.0 * stats->node_visits + 64.0 * stats->prim_tests +
-                                       128.0 * stats->medium_tests + 64.0 * stats->segments +
-                                       7.0 * 8.0 * 28.0 * stats->noise_evals + 32.0 * (double)nitems;
+            stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, (double)s->npix);
         }
     }
     return RT_OK;

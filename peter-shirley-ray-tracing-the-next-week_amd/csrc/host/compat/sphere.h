@@ -1,0 +1,3 @@
+// compat/sphere.h — reference header name; see rtnw_compat.h
+#pragma once
+#include "rtnw_compat.h"

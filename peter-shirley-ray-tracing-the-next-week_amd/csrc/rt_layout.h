@@ -76,6 +76,6 @@ struct rt_dmedium {
 
 // Counters of the RT_FLAG_COUNT kernel variant (uint64 each).
 enum {
-    RT_CNT_SAMPLES = 0, RT_CNT_SEGMENTS, RT_CNT_NODES, RT_CNT_PRIMS, RT_CNT_MEDIA, RT_CNT_NOISE,
-    RT_CNT_SHADES, RT_CNT_INSTANCED, RT_CNT_N
+    RT_CNT_SAMPLES = 0, RT_CNT_SEGMENTS, RT_CNT_NODES, RT_CNT_SPHERES, RT_CNT_MSPHERES, RT_CNT_RECTS,
+    RT_CNT_INSTANCED, RT_CNT_MEDIA, RT_CNT_SHADES, RT_CNT_NOISE, RT_CNT_N
 };

@@ -84,8 +84,9 @@ class RtRenderParams(ctypes.Structure):
 
 
 class RtStats(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_double) for n in ("samples", "segments", "node_visits", "prim_tests", "medium_tests",
-                                               "noise_evals", "algorithmic_bytes", "kernel_ms", "resolve_ms")]
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "samples", "segments", "node_visits", "sphere_tests", "moving_sphere_tests", "rect_tests", "instanced_tests",
+        "medium_tests", "shades", "noise_evals", "algorithmic_bytes", "kernel_ms", "resolve_ms")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -157,8 +157,11 @@ def test_count_mode_statistics():
     segs = st2["segments"] / st2["samples"]
     _, ost = O.render(O.kernel_spec("final", nx, ny, ns, seed=1, threads=THREADS))
     assert abs(segs - ost["segments"] / ost["samples"]) < 1e-9       # same paths as the oracle
-    assert st2["node_visits"] > st2["segments"] and st2["prim_tests"] > 0
+    assert st2["node_visits"] > st2["segments"] and st2["rect_tests"] > 0 and st2["moving_sphere_tests"] > 0
     assert st2["medium_tests"] == 2 * st2["segments"]
+    # every medium evaluation tests its one boundary sphere at least once
+    assert st2["sphere_tests"] > st2["medium_tests"]
+    assert st2["instanced_tests"] == 0 and st2["noise_evals"] > 0 and st2["shades"] <= st2["segments"]
     assert st["kernel_ms"] > 0
 
 

@@ -25,8 +25,17 @@ for step in "$@"; do
     testsk) run tests 1200 python -m pytest tests -m gpu -q -s ;;
     bench_small) run bench_small 600 python bench.py --spp 64 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench)  run bench 900 python bench.py ;;
-    prof)   cd /tmp; export TMPDIR=/tmp; cd - >/dev/null
-            run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --spp 256 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prof)   export TMPDIR=/tmp
+            run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    counters) export TMPDIR=/tmp; run counters 120 rocprofv3 -L ;;
+    pmc_fetch) export TMPDIR=/tmp
+            run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmc_write) export TMPDIR=/tmp
+            run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmc_l2) export TMPDIR=/tmp
+            run pmc_l2 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmc_sq) export TMPDIR=/tmp
+            run pmc_sq 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
