@@ -132,7 +132,10 @@ int rt_camera_init(rt_camera_desc *out, const float lookfrom[3], const float loo
 
 /* ------------------------------------------------------------------ render */
 enum { RT_BG_BLACK = 0, RT_BG_SKY = 1 };
-enum { RT_FLAG_COUNT = 1 };       /* run the counting variant: fills the rt_stats visit counters */
+enum {
+    RT_FLAG_COUNT = 1,            /* counting variant: fills the rt_stats visit counters */
+    RT_FLAG_PROFILE = 2           /* stamp variant: fills cycles_* (diagnostic; never timed) */
+};
 
 typedef struct rt_render_params {
     int32_t nx, ny;               /* full image (u,v normalisation and pixel keys) */
@@ -161,6 +164,11 @@ typedef struct rt_stats {
     double algorithmic_bytes;     /* SURVEY §8d byte model for the launch (RT_FLAG_COUNT) */
     double kernel_ms;             /* megakernel time from HIP events on the render stream */
     double resolve_ms;            /* partial-sum resolve kernel time */
+    double cycles_claim;          /* RT_FLAG_PROFILE: wave cycles in work claim + camera sampling */
+    double cycles_traverse;       /*   ... in the BVH / primitive search */
+    double cycles_media;          /*   ... in constant_medium evaluation + hit record */
+    double cycles_shade;          /*   ... in material / texture evaluation */
+    double grid;                  /* workgroups launched (persistent grid) */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */

@@ -39,7 +39,7 @@ struct RtKernelArgs {
     unsigned long long *stats;  // RT_CNT_N counters (count variant)
 };
 
-extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, bool count, hipStream_t stream);
+extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
-extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, bool count);
+extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode);  // mode: 0 plain, 1 count, 2 profile

@@ -30,7 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../rt_layout.h"
+#include "rt_layout.h"
 #include "rt_kernel.h"
 
 #define RT_FLT_MAX 0x1.fffffep+127f
@@ -70,14 +70,29 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed, uint32_t pixel, ui
 }
 struct Rng {
     uint64_t key;
+    uint64_t mkey;   // medium stream key, derived once per sample
     uint32_t n;
+    __device__ __forceinline__ void start(uint64_t k) { key = k; n = 0; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
     __device__ __forceinline__ double next() { ++n; return u48(mix64(key + (uint64_t)n * kGamma)); }
     __device__ __forceinline__ double medium(int bounce, int k) const {
-        uint64_t mkey = mix64(key ^ 0xD1B54A32D192ED03ull);
         uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
         return u48(mix64(mkey + (m + 1) * kGamma));
     }
 };
+
+// pow(x, 5.0) for the x = (double)(float) of schlick (material.h:19).  x has 24
+// significant bits, so x*x is exact; x^4 and x^5 are carried as double-double and
+// rounded once: the double result is the correctly rounded x^5 except in
+// vanishingly rare near-ties, i.e. what glibc's pow returns, at a fraction of
+// ocml's general pow cost (and register pressure).
+__device__ __forceinline__ double pow5(double x) {
+    const double x2 = x * x;
+    const double x4h = x2 * x2;
+    const double x4l = __builtin_fma(x2, x2, -x4h);
+    const double p = x4h * x;
+    const double pe = __builtin_fma(x4h, x, -p);
+    return p + (pe + x4l * x);
+}
 
 // ----------------------------------------------------------- scene access
 __device__ __forceinline__ float4 ld4(const float4 *p, uint32_t i) { return p[i]; }
@@ -150,18 +165,22 @@ __device__ __forceinline__ V3 msphere_center(float4 g0, float4 g1, float4 g2, fl
     return add(mk(g0.x, g0.y, g0.z), scale((time - g1.w) / g2.x, mk(g1.x, g1.y, g1.z)));
 }
 
-__device__ __forceinline__ float rect_t(int axis, float4 g0, float k, const Ray &r, float tmin) {   // aarect.h:50-100
-    float oa = axis == 0 ? r.o.x : (axis == 1 ? r.o.y : r.o.z);
-    float da = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
+// One rect test for a plane axis (aarect.h:50-100); oa/da: ray along the plane
+// normal, (oi, di) and (oj, dj): the two in-plane axes.  Written once per kind
+// with direct field reads so the compiler never indexes the ray through memory.
+__device__ __forceinline__ float plane_t(float oa, float da, float oi, float di, float oj, float dj, float4 g0, float k,
+                                         float tmin) {
     float t = (k - oa) / da;
     if (t < tmin || t > RT_FLT_MAX) return RT_INF;
-    // in-plane axes: xy -> (x, y); xz -> (x, z); yz -> (y, z)
-    float oi = axis == 0 ? r.o.y : r.o.x, di = axis == 0 ? r.d.y : r.d.x;
-    float oj = axis == 2 ? r.o.y : r.o.z, dj = axis == 2 ? r.d.y : r.d.z;
     float a = oi + t * di;
     float b = oj + t * dj;
     if (a < g0.x || a > g0.y || b < g0.z || b > g0.w) return RT_INF;
     return t;
+}
+__device__ __forceinline__ float rect_t(int kind, float4 g0, float k, const Ray &r, float tmin) {
+    if (kind == RT_PRIM_XY_RECT) return plane_t(r.o.z, r.d.z, r.o.x, r.d.x, r.o.y, r.d.y, g0, k, tmin);
+    if (kind == RT_PRIM_XZ_RECT) return plane_t(r.o.y, r.d.y, r.o.x, r.d.x, r.o.z, r.d.z, g0, k, tmin);
+    return plane_t(r.o.x, r.d.x, r.o.y, r.d.y, r.o.z, r.d.z, g0, k, tmin);
 }
 
 // prim kinds: 0 sphere, 1 moving sphere, 2 xy, 3 xz, 4 yz  (rect axis = 2, 1, 0)
@@ -187,7 +206,7 @@ __device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, ui
         t = sphere_t(msphere_center(g0, g1, g2, r.time), g0.w, r, tmin);
         key = order;
     } else {
-        t = rect_t(rect_axis(kind), g0, g1.x, r, tmin);
+        t = rect_t(kind, g0, g1.x, r, tmin);
         key = -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
     }
     return t;
@@ -283,6 +302,7 @@ __device__ float perlin_turb(const float4 *ranvec, const int *perm, V3 p) {   //
     float accum = 0;
     V3 temp_p = p;
     float weight = 1.0f;
+#pragma unroll 1
     for (int i = 0; i < 7; i++) {
         accum += weight * perlin_noise(ranvec, perm, temp_p);
         weight = (float)((double)weight * 0.5);
@@ -332,8 +352,14 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 
 constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
 
-template <bool kCount>
-__global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
+#ifndef RT_WAVES_PER_SIMD
+#define RT_WAVES_PER_SIMD 1
+#endif
+
+// kCount: visit counters (RT_FLAG_COUNT).  kProf: wave-level s_memtime stamps per
+// stage (RT_FLAG_PROFILE, a diagnostic build whose timing is never quoted).
+template <bool kCount, bool kProf>
+__global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     const uint32_t lane = lane_id();
     uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
@@ -351,10 +377,19 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
     r.o = mk(0, 0, 0); r.d = mk(0, 0, 0); r.time = 0;
     V3 beta = mk(1, 1, 1);
     int depth = 0;
-    Rng g; g.key = 0; g.n = 0;
+    Rng g; g.key = 0; g.mkey = 0; g.n = 0;
     uint32_t px = 0, py = 0;
 
     Counters cnt;
+    uint64_t prof[4] = {0, 0, 0, 0};
+    uint64_t stamp = kProf ? __builtin_amdgcn_s_memtime() : 0;
+    auto mark = [&](int k) {
+        if (kProf) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            prof[k] += now - stamp;
+            stamp = now;
+        }
+    };
 
 
     for (;;) {
@@ -398,8 +433,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
         // ---- 2. start a camera sample (main.cpp:305-308, camera.h:41-56) -----
         if (!path && !finished) {
             int j = A.ny - 1 - (int)py;
-            g.key = sample_key(A.seed, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset);
-            g.n = 0;
+            g.start(sample_key(A.seed, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
             float u = (float)((double)(int)px + g.next()) / (float)A.nx;
             float v = (float)((double)j + g.next()) / (float)A.ny;
             V3 p;
@@ -423,6 +457,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
             if (kCount) cnt.samples++;
         }
 
+        mark(0);
         if (!path) continue;   // finished lanes idle until the wave drains
 
         // ---- 3. closest surface hit: BVH2, stack in LDS ------------------------
@@ -482,6 +517,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
             }
         }
 
+        mark(1);
         // ---- 4. media after the surfaces (constant_medium.h:26-50) -------------
         bool have = best_prim != 0xFFFFFFFFu;
         Hit hr;
@@ -489,10 +525,33 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
         for (int k = 0; k < A.nmedia; ++k) {
             if (kCount) cnt.media++;
             const int4 md = A.media[k];
-            float r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
-            if (r1 == RT_INF) continue;
-            float r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
-            if (r2 == RT_INF) continue;
+            float r1, r2;
+            const float4 bm = A.bprims[md.x * 4 + 3];
+            if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {
+                // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
+                if (kCount) cnt.spheres++;
+                const float4 sg = A.bprims[md.x * 4 + 0];
+                V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
+                float a = dot(r.d, r.d);
+                float b = dot(oc, r.d);
+                float cc = dot(oc, oc) - sg.w * sg.w;
+                float disc = b * b - a * cc;
+                if (!(disc > 0)) continue;
+                const float ta = (-b - sqrtf(disc)) / a;
+                const float tb = (-b + sqrtf(disc)) / a;
+                if (ta < RT_FLT_MAX && ta > -RT_FLT_MAX) r1 = ta;
+                else if (tb < RT_FLT_MAX && tb > -RT_FLT_MAX) r1 = tb;
+                else continue;
+                const float tmin2 = (float)((double)r1 + 0.0001);
+                if (ta < RT_FLT_MAX && ta > tmin2) r2 = ta;
+                else if (tb < RT_FLT_MAX && tb > tmin2) r2 = tb;
+                else continue;
+            } else {
+                r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
+                if (r1 == RT_INF) continue;
+                r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
+                if (r2 == RT_INF) continue;
+            }
             float tmax = have ? best_t : RT_FLT_MAX;
             if (r1 < A.tmin) r1 = A.tmin;
             if (r2 > tmax) r2 = tmax;
@@ -511,6 +570,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
             }
         }
 
+        mark(2);
         // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
         V3 L;
         bool terminate = true;
@@ -574,7 +634,7 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
                         // schlick, material.h:16-20
                         float r0 = (1 - ref_idx) / (1 + ref_idx);
                         r0 = r0 * r0;
-                        reflect_prob = (float)(r0 + (double)(1 - r0) * pow((double)(1 - cosine), 5.0));
+                        reflect_prob = (float)(r0 + (double)(1 - r0) * pow5((double)(1 - cosine)));
                     } else {
                         reflect_prob = 1.0f;
                     }
@@ -604,7 +664,10 @@ __global__ __launch_bounds__(RT_BLOCK) void rt_megakernel(RtKernelArgs A) {
             ++s_cur;
             path = false;
         }
+        mark(3);
     }
+    if (kProf && lane == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_CNT_N + k], (unsigned long long)prof[k]);
 
     if (kCount) {
         uint64_t v[RT_CNT_N] = {cnt.samples, cnt.segments, cnt.nodes, cnt.spheres, cnt.mspheres, cnt.rects,
@@ -637,11 +700,13 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
 }  // namespace
 
 // --------------------------------------------------------------- launchers
-extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, bool count, hipStream_t stream) {
-    if (count)
-        hipLaunchKernelGGL(rt_megakernel<true>, dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
+    if (mode == 1)
+        hipLaunchKernelGGL((rt_megakernel<true, false>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+    else if (mode == 2)
+        hipLaunchKernelGGL((rt_megakernel<false, true>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else
-        hipLaunchKernelGGL(rt_megakernel<false>, dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, false>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     return hipGetLastError();
 }
 
@@ -652,8 +717,10 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
     return hipGetLastError();
 }
 
-extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, bool count) {
-    if (count)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false>, RT_BLOCK, 0);
+extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode) {
+    if (mode == 1)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false>, RT_BLOCK, 0);
+    if (mode == 2)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false>, RT_BLOCK, 0);
 }

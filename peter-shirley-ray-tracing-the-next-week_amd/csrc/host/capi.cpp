@@ -91,7 +91,7 @@ double algorithmic_bytes(const rt_stats &st, double items, double pixels) {
 struct rt_scene {
     int device = 0;
     int cus = 0;
-    int grid = 0, grid_count = 0;
+    int grid[3] = {0, 0, 0};   // persistent grid per kernel variant (plain, count, profile)
     hipStream_t own_stream = nullptr;
     // scene in HBM
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
@@ -311,13 +311,14 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return cleanup(hip_fail(e, "hipGetDeviceProperties"));
     s->cus = prop.multiProcessorCount;
-    int bpc = 0, bpc_count = 0;
-    if ((e = rt_megakernel_occupancy(&bpc, false)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
-    if ((e = rt_megakernel_occupancy(&bpc_count, true)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
-    s->grid = std::max(1, bpc) * s->cus;
-    s->grid_count = std::max(1, bpc_count) * s->cus;
+    for (int mode = 0; mode < 3; mode++) {
+        int bpc = 0;
+        if ((e = rt_megakernel_occupancy(&bpc, mode)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+        s->grid[mode] = std::max(1, bpc) * s->cus;
+    }
     if ((e = hipMalloc(&s->counter, 64)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc counter"));
-    if ((e = hipMalloc(&s->stats, RT_CNT_N * sizeof(unsigned long long))) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc stats"));
+    if ((e = hipMalloc(&s->stats, (RT_CNT_N + 4) * sizeof(unsigned long long))) != hipSuccess)
+        return cleanup(hip_fail(e, "hipMalloc stats"));
     for (auto &ev : s->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
     if ((e = hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking)) != hipSuccess)
@@ -379,8 +380,10 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         s->slab_bytes = slab_bytes;
     }
     const bool count = (p->flags & RT_FLAG_COUNT) != 0;
+    const bool prof = !count && (p->flags & RT_FLAG_PROFILE) != 0;
+    const int mode = count ? 1 : (prof ? 2 : 0);
     HIP_TRY(hipMemsetAsync(s->counter, 0, 64, stream));
-    if (count) HIP_TRY(hipMemsetAsync(s->stats, 0, RT_CNT_N * sizeof(unsigned long long), stream));
+    if (count || prof) HIP_TRY(hipMemsetAsync(s->stats, 0, (RT_CNT_N + 4) * sizeof(unsigned long long), stream));
 
     RtKernelArgs a{};
     a.nodes = (const float4 *)s->nodes;
@@ -425,7 +428,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
 
     const float k = (float)(1.0 / (double)(float)p->spp);   // vec3::operator/= (vec3.h:134-141)
     HIP_TRY(hipEventRecord(s->ev[0], stream));
-    HIP_TRY(rt_launch_megakernel(&a, count ? s->grid_count : s->grid, count, stream));
+    HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
     HIP_TRY(hipEventRecord(s->ev[1], stream));
     HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, nchunks, k, (const uint32_t *)s->job_out, out_dev, stream));
     HIP_TRY(hipEventRecord(s->ev[2], stream));
@@ -454,6 +457,15 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->noise_evals = (double)c[RT_CNT_NOISE];
             stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, (double)s->npix);
         }
+        if (prof) {
+            unsigned long long c[RT_CNT_N + 4];
+            HIP_TRY(hipMemcpy(c, s->stats, sizeof c, hipMemcpyDeviceToHost));
+            stats->cycles_claim = (double)c[RT_CNT_N + 0];
+            stats->cycles_traverse = (double)c[RT_CNT_N + 1];
+            stats->cycles_media = (double)c[RT_CNT_N + 2];
+            stats->cycles_shade = (double)c[RT_CNT_N + 3];
+        }
+        stats->grid = (double)s->grid[mode];
     }
     return RT_OK;
 }

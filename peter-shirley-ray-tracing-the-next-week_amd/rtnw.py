@@ -20,12 +20,13 @@ import re
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librt_hip.so")
+LIB_PATH = os.environ.get("RTNW_LIB") or os.path.join(HERE, "librt_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "rt_hip.h")
 
 RT_OK = 0
 RT_BG_BLACK, RT_BG_SKY = 0, 1
 RT_FLAG_COUNT = 1
+RT_FLAG_PROFILE = 2
 
 
 class RtError(RuntimeError):
@@ -86,7 +87,8 @@ class RtRenderParams(ctypes.Structure):
 class RtStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_double) for n in (
         "samples", "segments", "node_visits", "sphere_tests", "moving_sphere_tests", "rect_tests", "instanced_tests",
-        "medium_tests", "shades", "noise_evals", "algorithmic_bytes", "kernel_ms", "resolve_ms")]
+        "medium_tests", "shades", "noise_evals", "algorithmic_bytes", "kernel_ms", "resolve_ms",
+        "cycles_claim", "cycles_traverse", "cycles_media", "cycles_shade", "grid")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -36,6 +36,9 @@ for step in "$@"; do
             run pmc_l2 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     pmc_sq) export TMPDIR=/tmp
             run pmc_sq 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    ab)     run ab 1200 python3 tools/ab.py peter-shirley-ray-tracing-the-next-week_amd/librt_hip.so variants/w3/librt_hip.so variants/w4/librt_hip.so --rounds 2 ;;
+    stages) run stages 600 python3 tools/stage_profile.py final ;;
+    stages_cornell) run stages_cornell 600 python3 tools/stage_profile.py cornell_box ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""tools/stage_profile.py — where the megakernel's wave-cycles go (RT_FLAG_PROFILE
+build: s_memtime stamps at the stage boundaries of each loop iteration, summed
+over waves).  Diagnostic only: shares, never timings."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "peter-shirley-ray-tracing-the-next-week_amd"))
+import rtnw  # noqa: E402
+
+scene_name = sys.argv[1] if len(sys.argv) > 1 else "final"
+nx, ny, spp = (500, 500, 256) if scene_name == "final" else (400, 400, 64)
+cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
+sc = rtnw.Scene.builtin(scene_name)
+cam = rtnw.Camera.preset(cam_name, nx, ny)
+out = {}
+for label, flags in (("plain", 0), ("profile", rtnw.RT_FLAG_PROFILE), ("count", rtnw.RT_FLAG_COUNT)):
+    p = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, flags=flags, seed=7)
+    _, st = sc.render_tile(cam, p, 0, 0, nx, ny, stats=True)
+    out[label] = st
+pr = out["profile"]
+tot = sum(pr[k] for k in ("cycles_claim", "cycles_traverse", "cycles_media", "cycles_shade"))
+shares = {k: pr[k] / tot for k in ("cycles_claim", "cycles_traverse", "cycles_media", "cycles_shade")}
+c = out["count"]
+print(json.dumps({"scene": scene_name, "image": [nx, ny], "spp": spp, "plain_kernel_ms": out["plain"]["kernel_ms"],
+                  "profile_kernel_ms": pr["kernel_ms"], "stage_share": shares,
+                  "per_ray": {k: c[k] / max(1, c["segments"]) for k in
+                              ("node_visits", "sphere_tests", "moving_sphere_tests", "rect_tests", "instanced_tests",
+                               "medium_tests", "shades", "noise_evals")},
+                  "rays_per_sample": c["segments"] / c["samples"], "grid": out["plain"]["grid"]}, indent=1))
