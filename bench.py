@@ -11,8 +11,10 @@ resident in HBM); the PPM write is not part of a step.
 
 Multi-GPU (torchrun, one process per GPU): weak scaling — N ranks render an image
 of N x 250,000 pixels (500x500, 1000x500, 1000x1000 = config 5's image, 2000x1000),
-interleaved 32x32 tiles (tile k -> rank k % N), then one torch.distributed gather
-(backend "nccl" = RCCL over xGMI) of the packed float tiles to rank 0.
+32x32 tiles interleaved diagonally (tile (tx, ty) -> rank (tx + ty) % N), then one
+torch.distributed gather (backend "nccl" = RCCL over xGMI) of the packed float
+tiles to rank 0.  `--dist-backend gloo` gathers through host memory instead, so the
+multi-rank path can be rehearsed with several ranks on one GPU.
 
 Prints ONE JSON line (rank 0) with roofline (algorithmic bytes / kernel time vs
 8 TB/s HBM) and cpu_baseline (the reference binary on host cores, bounded sample).
@@ -85,16 +87,18 @@ def cpu_baseline(budget_procs):
                       f"{st['seconds']:.2f}s"}
 
 
-def read_traffic(workload):
+def read_traffic(samples_per_launch):
+    """HBM bytes per launch from the committed PMC measurement (profiles/traffic.json,
+    written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3
+    passes of this workload, FETCH_SIZE doubled per the gfx950 correction), scaled to
+    this launch's sample count."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
-        if t.get("workload") == workload:
-            return t.get("hbm_bytes_per_launch")
+        return t["hbm_bytes_per_sample"] * samples_per_launch
     except Exception:
-        pass
-    return None
+        return None
 
 
 def main():
@@ -106,36 +110,41 @@ def main():
     ap.add_argument("--chunk", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ppm", default="")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", gpu)
 
     nx, ny = image_for(world)
     spp = args.spp
-    tiles = rtnw.tiles_for_rank(nx, ny, TILE, rank, world) if world > 1 else [(0, 0, nx, ny)]
-    all_counts = [sum(w * h for _, _, w, h in rtnw.tiles_for_rank(nx, ny, TILE, r, world)) * 3 for r in range(world)] \
-        if world > 1 else [nx * ny * 3]
-    n_local = all_counts[rank]
+    if world > 1:
+        all_tiles, all_counts = rtnw.rank_layout(nx, ny, TILE, world)
+    else:
+        all_tiles, all_counts = [[(0, 0, nx, ny)]], [nx * ny * 3]
+    tiles = all_tiles[rank]
     n_max = max(all_counts)
 
-    scene = rtnw.Scene.builtin("final", device=local)
+    scene = rtnw.Scene.builtin("final", device=gpu)
     cam = rtnw.Camera.preset("cornell", nx, ny)
     params = rtnw.RenderParams(nx, ny, spp, max_depth=50, chunk=args.chunk, seed=2024)
     out = torch.zeros(n_max, dtype=torch.float32, device=dev)
-    gather_list = [torch.empty(n_max, dtype=torch.float32, device=dev) for _ in range(world)] \
+    gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    gather_list = [torch.empty(n_max, dtype=torch.float32, device=gdev) for _ in range(world)] \
         if (world > 1 and rank == 0) else None
 
     def step():
         stream = torch.cuda.current_stream(dev).cuda_stream
         st = scene.render_tiles(cam, params, tiles, out.data_ptr(), stream, stats=True)
         if world > 1:
-            dist.gather(out, gather_list, dst=0)
+            dist.gather(out if args.dist_backend == "nccl" else out.cpu(), gather_list, dst=0)
         return st
 
     workload = f"c4: final() {nx}x{ny} pixels x {spp} spp, depth 50" + (f" over {world} GPUs" if world > 1 else "")
@@ -174,8 +183,13 @@ def main():
     alg = cst["algorithmic_bytes"]
     achieved = alg / avg_kernel_s / 1e9
 
-    if rank == 0 and args.ppm and world == 1:
-        img = out[: nx * ny * 3].cpu().numpy().reshape(ny, nx, 3)
+    if rank == 0 and args.ppm:
+        if world == 1:
+            img = out[: nx * ny * 3].cpu().numpy().reshape(ny, nx, 3)
+        else:   # the last timed step's gathered tiles, unpacked on the root
+            img = np.zeros((ny, nx, 3), np.float32)
+            for r in range(world):
+                rtnw.unpack_tiles(gather_list[r][: all_counts[r]].cpu().numpy(), all_tiles[r], img)
         with open(args.ppm, "wb") as f:
             f.write(rtnw.ppm_text(rtnw.quantize(img)))
 
@@ -197,7 +211,7 @@ def main():
                        "tile": TILE if world > 1 else None, "chunk": args.chunk,
                        "parallelism": f"pixel tiles x{world}" + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(workload),
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(len(tiles) and sum(w * h for _, _, w, h in tiles) * spp),
                          "kernel_ms_avg": avg_kernel_s * 1e3,
                          "algorithmic_bytes_per_launch": alg,
                          "rays_per_sample": cst["segments"] / max(1.0, cst["samples"]),

@@ -282,10 +282,10 @@ __device__ float perlin_noise(const float4 *ranvec, const int *perm, V3 p) {   /
     float uu = u * u * (3 - 2 * u);
     float vv = v * v * (3 - 2 * v);
     float ww = w * w * (3 - 2 * w);
-    float accum = 0;
-#pragma unroll
+    float accum = 0;   // corner order i, j, k as perlin_interp sums them
+#pragma unroll 1
     for (int a = 0; a < 2; a++)
-#pragma unroll
+#pragma unroll 1
         for (int b = 0; b < 2; b++)
 #pragma unroll
             for (int d = 0; d < 2; d++) {
@@ -352,8 +352,11 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 
 constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
 
+// Minimum waves per SIMD the register allocation must allow (launch_bounds second
+// argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  Traversal is latency-bound, so
+// occupancy wins over the few spilled dwords: tools/ab.py, profiles/r01.
 #ifndef RT_WAVES_PER_SIMD
-#define RT_WAVES_PER_SIMD 1
+#define RT_WAVES_PER_SIMD 4
 #endif
 
 // kCount: visit counters (RT_FLAG_COUNT).  kProf: wave-level s_memtime stamps per

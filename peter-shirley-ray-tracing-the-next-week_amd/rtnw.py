@@ -295,12 +295,28 @@ def ppm_text(rgb: np.ndarray) -> bytes:
 
 
 def tiles_for_rank(nx, ny, tile, rank, world):
-    """Interleaved tile assignment: tile k (row-major over the image) goes to rank k % world."""
+    """Diagonal interleave: tile (tx, ty) goes to rank (tx + ty) % world.  Neighbouring
+    tiles land on different ranks (spatially varying path cost evens out) and the
+    narrow edge tiles rotate over the ranks (pixel counts balance)."""
     out = []
-    k = 0
-    for y0 in range(0, ny, tile):
-        for x0 in range(0, nx, tile):
-            if k % world == rank:
+    for ty, y0 in enumerate(range(0, ny, tile)):
+        for tx, x0 in enumerate(range(0, nx, tile)):
+            if (tx + ty) % world == rank:
                 out.append((x0, y0, min(tile, nx - x0), min(tile, ny - y0)))
-            k += 1
     return out
+
+
+def rank_layout(nx, ny, tile, world):
+    """Tiles and packed float counts of every rank (interleaved assignment)."""
+    tiles = [tiles_for_rank(nx, ny, tile, r, world) for r in range(world)]
+    counts = [sum(w * h for _, _, w, h in t) * 3 for t in tiles]
+    return tiles, counts
+
+
+def unpack_tiles(packed, tiles, img):
+    """Scatters one rank's packed tiles (as rt_render_tiles writes them) into img [ny, nx, 3]."""
+    off = 0
+    for x0, y0, w, h in tiles:
+        img[y0:y0 + h, x0:x0 + w] = np.asarray(packed[off:off + w * h * 3]).reshape(h, w, 3)
+        off += w * h * 3
+    return img

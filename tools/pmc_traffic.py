@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""tools/pmc_traffic.py OUTDIR PROFILE_DIR — summarises rocprofv3 PMC passes of bench.py.
+
+Reads OUTDIR/pmc_{fetch,write,l2,sq}/run_counter_collection.csv (separate passes, as
+MI355X_MICROARCH.md §rocprofv3 requires: FETCH_SIZE and WRITE_SIZE do not fit one
+pass), keeps the dispatches of the timed megakernel (rt_megakernel<false, false>),
+and writes:
+  PROFILE_DIR/traffic.json  hbm_bytes_per_launch / _per_sample for bench.py's roofline
+  PROFILE_DIR/pmc_summary.md
+HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE/WRITE_SIZE are in KiB and
+gfx950's FETCH_SIZE reports half the bytes of wide reads (MI355X_MICROARCH.md §HBM);
+the doubling is uncalibrated for this kernel's scattered 16-B reads, so the read
+side is an upper estimate.
+"""
+import csv
+import json
+import os
+import sys
+
+KERNEL = os.environ.get("RT_PMC_KERNEL", "rt_megakernel<false, false>")
+
+
+def load(path):
+    rows = {}
+    if not os.path.exists(path):
+        return rows
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if KERNEL not in r["Kernel_Name"]:
+                continue
+            d = rows.setdefault(r["Dispatch_Id"], {"dur_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                                                   "grid": int(r["Grid_Size"]), "vgpr": int(r["VGPR_Count"]),
+                                                   "scratch": int(r["Scratch_Size"])})
+            d[r["Counter_Name"]] = float(r["Counter_Value"])
+    return rows
+
+
+def first(rows):
+    return next(iter(rows.values())) if rows else {}
+
+
+def main():
+    out, prof = sys.argv[1], sys.argv[2]
+    samples = float(sys.argv[3]) if len(sys.argv) > 3 else 500 * 500 * 1000
+    fetch = first(load(os.path.join(out, "pmc_fetch", "run_counter_collection.csv")))
+    write = first(load(os.path.join(out, "pmc_write", "run_counter_collection.csv")))
+    l2 = first(load(os.path.join(out, "pmc_l2", "run_counter_collection.csv")))
+    sq = first(load(os.path.join(out, "pmc_sq", "run_counter_collection.csv")))
+    res = {"workload": "c4: final() 500x500 x 1000 spp (bench.py defaults)", "samples_per_launch": samples}
+    if fetch and write:
+        fb = fetch["FETCH_SIZE"] * 1024.0
+        wb = write["WRITE_SIZE"] * 1024.0
+        res.update(fetch_size_bytes=fb, write_size_bytes=wb, hbm_bytes_per_launch=2 * fb + wb,
+                   hbm_bytes_per_sample=(2 * fb + wb) / samples, kernel_ns=fetch["dur_ns"])
+    if l2:
+        res["l2_hit_rate"] = l2["TCC_HIT_sum"] / (l2["TCC_HIT_sum"] + l2["TCC_MISS_sum"])
+    if sq:
+        res["valu_active_per_wave_cycle"] = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
+        res["wait_any_per_wave_cycle"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
+        res["wait_inst_any_per_wave_cycle"] = sq["SQ_WAIT_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
+        res["valu_insts_per_sample_wave"] = sq["SQ_INSTS_VALU"] * 64 / samples
+        res["effective_clock_ghz"] = sq["GRBM_GUI_ACTIVE"] / 8 / sq["dur_ns"]
+        res["waves"] = sq["SQ_WAVES"]
+        res["vgpr"] = sq["vgpr"]
+        res["scratch_bytes_per_lane"] = sq["scratch"]
+    os.makedirs(prof, exist_ok=True)
+    with open(os.path.join(prof, "traffic.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    lines = ["# PMC summary (timed megakernel, separate rocprofv3 passes)", ""]
+    lines += [f"- {k}: {v:.4g}" if isinstance(v, float) else f"- {k}: {v}" for k, v in res.items()]
+    with open(os.path.join(prof, "pmc_summary.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
