@@ -169,6 +169,11 @@ typedef struct rt_stats {
     double cycles_media;          /*   ... in constant_medium evaluation + hit record */
     double cycles_shade;          /*   ... in material / texture evaluation */
     double grid;                  /* workgroups launched (persistent grid) */
+    double wave_iterations;       /* RT_FLAG_COUNT: megakernel loop iterations, summed over waves */
+    double wave_node_trips;       /*   wave-level BVH node steps (SIMD efficiency = node_visits / 64x this) */
+    double wave_prim_trips;       /*   wave-level primitive-test steps */
+    double wave_sphere_draw_trips;/*   wave-level random_in_unit_sphere rejection rounds */
+    double lane_sphere_draw_trips;/*   lane-level rejection rounds */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */
@@ -188,7 +193,7 @@ int rt_render_tile(rt_scene *s, const rt_camera_desc *cam, const rt_render_param
  * out_dev receives the tiles packed back to back (tile k at offset sum_{i<k} w_i*h_i*3
  * floats, each row-major).  Enqueued on `stream` (a hipStream_t; NULL = default
  * stream).  When stats is non-NULL the call waits for completion to read the
- * HIP-event timings. */
+ * HIP-event timings.  ntiles == 0 is a no-op (a rank without tiles). */
 int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p,
                     const int32_t *tiles, int ntiles, float *out_dev, void *stream, rt_stats *stats);
 

@@ -243,9 +243,15 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
 }
 
 // Closest boundary hit of a constant_medium (its own small list), t > / >= tmin.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask);
+// true on exactly one active lane: counts a wave-level event once per wave
+__device__ __forceinline__ bool first_active() { return lanes_below(__ballot(1)) == 0; }
+
 struct Counters {
     uint64_t samples = 0, segments = 0, nodes = 0, spheres = 0, mspheres = 0, rects = 0, instanced = 0, media = 0,
              shades = 0, noise = 0;
+    // wave-level trip counts (SIMD efficiency = lane-level count / (64 x wave-level count))
+    uint64_t w_iters = 0, w_nodes = 0, w_prims = 0, w_rius = 0, l_rius = 0;
     __device__ __forceinline__ void prim(int kind) {
         const int k = kind & 0xff;
         if (k == RT_PRIM_SPHERE) spheres++;
@@ -334,9 +340,11 @@ __device__ V3 tex_value(const RtKernelArgs &A, int ti, V3 p, Counters &cnt) {   
 }
 
 // --------------------------------------------------------------- scatter
-__device__ __forceinline__ V3 random_in_unit_sphere(Rng &g) {   // material.h:41-47
+template <bool kCount>
+__device__ __forceinline__ V3 random_in_unit_sphere(Rng &g, Counters &cnt) {   // material.h:41-47
     V3 p;
     do {
+        if (kCount) { cnt.l_rius++; if (first_active()) cnt.w_rius++; }
         double x = g.next(), y = g.next(), z = g.next();
         p = sub(scale(2.0f, mk((float)x, (float)y, (float)z)), mk(1, 1, 1));
     } while ((double)dot(p, p) >= 1.0);
@@ -461,6 +469,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         }
 
         mark(0);
+        if (kCount && first_active()) cnt.w_iters++;
         if (!path) continue;   // finished lanes idle until the wave drains
 
         // ---- 3. closest surface hit: BVH2, stack in LDS ------------------------
@@ -475,7 +484,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             int sp = 0;
             for (;;) {
                 if (!(node & RT_LEAF_BIT)) {
-                    if (kCount) cnt.nodes++;
+                    if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
                     const float4 b0 = A.nodes[node * 4 + 0];
                     const float4 b1 = A.nodes[node * 4 + 1];
                     const float4 b2 = A.nodes[node * 4 + 2];
@@ -508,7 +517,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                     for (uint32_t q = 0; q < nleaf; ++q) {
                         int key, kind;
                         float t = prim_t(A.prims, A.insts, first + q, r, A.tmin, key, kind);
-                        if (kCount) cnt.prim(kind);
+                        if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
                         if (t < best_t || (t == best_t && key < best_key)) {
                             best_t = t; best_key = key; best_prim = first + q;
                         }
@@ -599,13 +608,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             Ray ns;
             if (depth < A.max_depth) {
                 if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
-                    V3 target = add(add(hr.p, hr.n), random_in_unit_sphere(g));
+                    V3 target = add(add(hr.p, hr.n), random_in_unit_sphere<kCount>(g, cnt));
                     ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
                     att = tex_value<kCount>(A, tex, hr.p, cnt);
                     scattered = true;
                 } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
                     V3 reflected = reflect(unit(r.d), hr.n);
-                    ns.o = hr.p; ns.d = add(reflected, scale(m0.z, random_in_unit_sphere(g))); ns.time = 0.0f;
+                    ns.o = hr.p; ns.d = add(reflected, scale(m0.z, random_in_unit_sphere<kCount>(g, cnt))); ns.time = 0.0f;
                     att = mk(m1.x, m1.y, m1.z);
                     scattered = dot(ns.d, hr.n) > 0;
                 } else if (kind == RT_MAT_DIELECTRIC) {                       // material.h:90-120
@@ -645,7 +654,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                     ns.d = (g.next() < (double)reflect_prob) ? reflected : refracted;
                     scattered = true;
                 } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
-                    ns.o = hr.p; ns.d = random_in_unit_sphere(g); ns.time = 0.0f;
+                    ns.o = hr.p; ns.d = random_in_unit_sphere<kCount>(g, cnt); ns.time = 0.0f;
                     att = tex_value<kCount>(A, tex, hr.p, cnt);
                     scattered = true;
                 }
@@ -671,6 +680,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
     }
     if (kProf && lane == 0)
         for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_CNT_N + k], (unsigned long long)prof[k]);
+    if (kCount) {
+        uint64_t w[5] = {cnt.w_iters, cnt.w_nodes, cnt.w_prims, cnt.w_rius, cnt.l_rius};
+        for (int k = 0; k < 5; ++k) {
+            uint64_t x = w[k];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
+            if (lane == 0 && x) atomicAdd(&A.stats[RT_CNT_N + 4 + k], (unsigned long long)x);
+        }
+    }
 
     if (kCount) {
         uint64_t v[RT_CNT_N] = {cnt.samples, cnt.segments, cnt.nodes, cnt.spheres, cnt.mspheres, cnt.rects,

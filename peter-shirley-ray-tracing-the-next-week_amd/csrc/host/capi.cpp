@@ -317,7 +317,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         s->grid[mode] = std::max(1, bpc) * s->cus;
     }
     if ((e = hipMalloc(&s->counter, 64)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc counter"));
-    if ((e = hipMalloc(&s->stats, (RT_CNT_N + 4) * sizeof(unsigned long long))) != hipSuccess)
+    if ((e = hipMalloc(&s->stats, (RT_CNT_N + 16) * sizeof(unsigned long long))) != hipSuccess)
         return cleanup(hip_fail(e, "hipMalloc stats"));
     for (auto &ev : s->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
@@ -359,7 +359,12 @@ static int prepare_job(rt_scene *s, const int32_t *tiles, int ntiles, int nx, in
 
 int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p, const int32_t *tiles, int ntiles,
                     float *out_dev, void *stream_v, rt_stats *stats) {
-    if (!s || !cam || !p || !tiles || ntiles <= 0 || !out_dev) return fail(RT_ERR_INVALID, "rt_render_tiles: bad argument");
+    if (!s || !cam || !p || ntiles < 0) return fail(RT_ERR_INVALID, "rt_render_tiles: bad argument");
+    if (ntiles == 0) {   // a rank with no tiles (more ranks than tiles) has nothing to do
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
+    if (!tiles || !out_dev) return fail(RT_ERR_INVALID, "rt_render_tiles: null tiles or output");
     if (p->nx <= 0 || p->ny <= 0 || p->spp <= 0 || p->max_depth < 0) return fail(RT_ERR_INVALID, "bad render parameters");
     if (s->has_moving && (cam->time0 < s->time0 || cam->time1 > s->time1))
         return fail(RT_ERR_INVALID, "camera shutter outside the scene's time span (moving-sphere bounds)");
@@ -383,7 +388,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     const bool prof = !count && (p->flags & RT_FLAG_PROFILE) != 0;
     const int mode = count ? 1 : (prof ? 2 : 0);
     HIP_TRY(hipMemsetAsync(s->counter, 0, 64, stream));
-    if (count || prof) HIP_TRY(hipMemsetAsync(s->stats, 0, (RT_CNT_N + 4) * sizeof(unsigned long long), stream));
+    if (count || prof) HIP_TRY(hipMemsetAsync(s->stats, 0, (RT_CNT_N + 16) * sizeof(unsigned long long), stream));
 
     RtKernelArgs a{};
     a.nodes = (const float4 *)s->nodes;
@@ -456,6 +461,13 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->shades = (double)c[RT_CNT_SHADES];
             stats->noise_evals = (double)c[RT_CNT_NOISE];
             stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, (double)s->npix);
+            unsigned long long w[5];
+            HIP_TRY(hipMemcpy(w, (unsigned long long *)s->stats + RT_CNT_N + 4, sizeof w, hipMemcpyDeviceToHost));
+            stats->wave_iterations = (double)w[0];
+            stats->wave_node_trips = (double)w[1];
+            stats->wave_prim_trips = (double)w[2];
+            stats->wave_sphere_draw_trips = (double)w[3];
+            stats->lane_sphere_draw_trips = (double)w[4];
         }
         if (prof) {
             unsigned long long c[RT_CNT_N + 4];

@@ -116,6 +116,9 @@ def test_rank_sharding_gathers_to_single_gpu_image():
         for r in range(R):
             tiles = rtnw.tiles_for_rank(nx, ny, 16, r, R)
             n = sum(w * h for _, _, w, h in tiles) * 3
+            if n == 0:   # more ranks than tiles on this diagonal: nothing to render
+                assert sc.render_tiles(cam, p, [], 0)["samples"] == 0
+                continue
             dev = ctypes.c_void_p()
             assert L.rt_device_alloc(0, n * 4, ctypes.byref(dev)) == 0
             sc.render_tiles(cam, p, tiles, dev.value)

@@ -29,4 +29,14 @@ print(json.dumps({"scene": scene_name, "image": [nx, ny], "spp": spp, "plain_ker
                   "per_ray": {k: c[k] / max(1, c["segments"]) for k in
                               ("node_visits", "sphere_tests", "moving_sphere_tests", "rect_tests", "instanced_tests",
                                "medium_tests", "shades", "noise_evals")},
-                  "rays_per_sample": c["segments"] / c["samples"], "grid": out["plain"]["grid"]}, indent=1))
+                  "rays_per_sample": c["segments"] / c["samples"], "grid": out["plain"]["grid"],
+                  "simd_efficiency": {
+                      "iterations_per_lane_segment": c["wave_iterations"] * 64 / c["segments"],
+                      "node_steps": c["node_visits"] / (64 * c["wave_node_trips"]),
+                      "prim_steps": (c["sphere_tests"] + c["rect_tests"] + c["moving_sphere_tests"]
+                                     - c["medium_tests"]) / (64 * max(1, c["wave_prim_trips"])),
+                      "sphere_draw_rounds": c["lane_sphere_draw_trips"] / (64 * max(1, c["wave_sphere_draw_trips"])),
+                      "wave_node_steps_per_iteration": c["wave_node_trips"] / c["wave_iterations"],
+                      "wave_prim_steps_per_iteration": c["wave_prim_trips"] / c["wave_iterations"],
+                      "wave_sphere_draw_rounds_per_iteration": c["wave_sphere_draw_trips"] / c["wave_iterations"]}},
+                 indent=1))
