@@ -363,6 +363,11 @@ constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
 // Minimum waves per SIMD the register allocation must allow (launch_bounds second
 // argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  Traversal is latency-bound, so
 // occupancy wins over the few spilled dwords: tools/ab.py, profiles/r01.
+// BVH traversal loop shape: 0 = node loop + leaf loop (while-while), 1 = one step per trip (if-if).
+#ifndef RT_TRAVERSAL_IFIF
+#define RT_TRAVERSAL_IFIF 0
+#endif
+
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -482,6 +487,60 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             const float nox = -r.o.x * ix, noy = -r.o.y * iy, noz = -r.o.z * iz;
             uint32_t node = A.root;
             int sp = 0;
+#if RT_TRAVERSAL_IFIF
+            // if-if: every trip each lane does ONE step — a node step or one
+            // primitive test — so lanes in leaves and lanes in inner nodes share trips.
+            uint32_t lp = 0, le = 0;   // pending primitives of the open leaf
+            for (;;) {
+                if (node != RT_EMPTY_CHILD && (node & RT_LEAF_BIT)) {
+                    lp = RT_LEAF_FIRST(node);
+                    le = lp + RT_LEAF_COUNT(node);
+                    node = RT_EMPTY_CHILD;
+                }
+                if (lp < le) {
+                    int key, kind;
+                    float t = prim_t(A.prims, A.insts, lp, r, A.tmin, key, kind);
+                    if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
+                    if (t < best_t || (t == best_t && key < best_key)) {
+                        best_t = t; best_key = key; best_prim = lp;
+                    }
+                    ++lp;
+                } else {
+                    if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
+                    const float4 b0 = A.nodes[node * 4 + 0];
+                    const float4 b1 = A.nodes[node * 4 + 1];
+                    const float4 b2 = A.nodes[node * 4 + 2];
+                    const float4 cf = A.nodes[node * 4 + 3];
+                    const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
+                    float a0 = __builtin_fmaf(b0.x, ix, nox), a1 = __builtin_fmaf(b0.y, ix, nox);
+                    float a2 = __builtin_fmaf(b0.z, iy, noy), a3 = __builtin_fmaf(b0.w, iy, noy);
+                    float a4 = __builtin_fmaf(b1.x, iz, noz), a5 = __builtin_fmaf(b1.y, iz, noz);
+                    float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), A.tmin));
+                    float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), best_t));
+                    float e0 = __builtin_fmaf(b1.z, ix, nox), e1 = __builtin_fmaf(b1.w, ix, nox);
+                    float e2 = __builtin_fmaf(b2.x, iy, noy), e3 = __builtin_fmaf(b2.y, iy, noy);
+                    float e4 = __builtin_fmaf(b2.z, iz, noz), e5 = __builtin_fmaf(b2.w, iz, noz);
+                    float tn1 = fmaxf(fmaxf(fminf(e0, e1), fminf(e2, e3)), fmaxf(fminf(e4, e5), A.tmin));
+                    float tf1 = fminf(fminf(fmaxf(e0, e1), fmaxf(e2, e3)), fminf(fmaxf(e4, e5), best_t));
+                    bool h0 = tn0 <= tf0 && c0 != RT_EMPTY_CHILD;
+                    bool h1 = tn1 <= tf1 && c1 != RT_EMPTY_CHILD;
+                    if (h0 && h1) {
+                        uint32_t nearc = c0, farc = c1;
+                        if (tn1 < tn0) { nearc = c1; farc = c0; }
+                        stk[sp * 64] = farc;
+                        ++sp;
+                        node = nearc;
+                    } else {
+                        node = h0 ? c0 : (h1 ? c1 : RT_EMPTY_CHILD);
+                    }
+                }
+                if (lp >= le && node == RT_EMPTY_CHILD) {
+                    if (sp == 0) break;
+                    --sp;
+                    node = stk[sp * 64];
+                }
+            }
+#else
             for (;;) {
                 if (!(node & RT_LEAF_BIT)) {
                     if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
@@ -527,6 +586,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                 --sp;
                 node = stk[sp * 64];
             }
+#endif
         }
 
         mark(1);
@@ -601,20 +661,32 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             const float4 m1 = A.mats[hr.mat * 2 + 1];
             const int kind = fbits(m0.x);
             const int tex = fbits(m0.y);
-            V3 emitted = mk(0, 0, 0);
-            if (kind == RT_MAT_DIFFUSE_LIGHT) emitted = tex_value<kCount>(A, tex, hr.p, cnt);
+            // The per-material work that dominates (texture lookup, the rejection loop
+            // of random_in_unit_sphere) runs ONCE for every lane that needs it instead
+            // of once per material branch; each lane still makes exactly the draws its
+            // own material makes, in the same order (one material per lane).
+            const bool live = depth < A.max_depth;
+            const bool textured = kind == RT_MAT_DIFFUSE_LIGHT ||
+                                  (live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC));
+            V3 tv = mk(0, 0, 0);
+            if (textured) tv = tex_value<kCount>(A, tex, hr.p, cnt);          // texture.h / perlin.h
+            const bool wants_sphere = live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_METAL ||
+                                               kind == RT_MAT_ISOTROPIC);
+            V3 rius = mk(0, 0, 0);
+            if (wants_sphere) rius = random_in_unit_sphere<kCount>(g, cnt);   // material.h:41-47
+            V3 emitted = kind == RT_MAT_DIFFUSE_LIGHT ? tv : mk(0, 0, 0);
             bool scattered = false;
             V3 att = mk(0, 0, 0);
             Ray ns;
-            if (depth < A.max_depth) {
+            if (live) {
                 if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
-                    V3 target = add(add(hr.p, hr.n), random_in_unit_sphere<kCount>(g, cnt));
+                    V3 target = add(add(hr.p, hr.n), rius);
                     ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
-                    att = tex_value<kCount>(A, tex, hr.p, cnt);
+                    att = tv;
                     scattered = true;
                 } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
                     V3 reflected = reflect(unit(r.d), hr.n);
-                    ns.o = hr.p; ns.d = add(reflected, scale(m0.z, random_in_unit_sphere<kCount>(g, cnt))); ns.time = 0.0f;
+                    ns.o = hr.p; ns.d = add(reflected, scale(m0.z, rius)); ns.time = 0.0f;
                     att = mk(m1.x, m1.y, m1.z);
                     scattered = dot(ns.d, hr.n) > 0;
                 } else if (kind == RT_MAT_DIELECTRIC) {                       // material.h:90-120
@@ -654,8 +726,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                     ns.d = (g.next() < (double)reflect_prob) ? reflected : refracted;
                     scattered = true;
                 } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
-                    ns.o = hr.p; ns.d = random_in_unit_sphere<kCount>(g, cnt); ns.time = 0.0f;
-                    att = tex_value<kCount>(A, tex, hr.p, cnt);
+                    ns.o = hr.p; ns.d = rius; ns.time = 0.0f;
+                    att = tv;
                     scattered = true;
                 }
             }

@@ -12,6 +12,7 @@
 #include "bvh.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <stdexcept>
 
@@ -94,6 +95,7 @@ struct Item {
 };
 
 struct Builder {
+    int max_leaf = RT_MAX_LEAF;   // RTNW_BVH_MAX_LEAF overrides (<= RT_MAX_LEAF), for experiments
     std::vector<Item> items;
     std::vector<rt_dnode> nodes;
     std::vector<int> order;   // leaf order -> original prim index
@@ -145,7 +147,7 @@ struct Builder {
         for (int k = 0; k < 3; k++) if (cb.hi[k] - cb.lo[k] > ext) { ext = cb.hi[k] - cb.lo[k]; axis = k; }
 
         if (force_median || ext <= 0) {
-            if (n <= RT_MAX_LEAF && !force_median) return -1;
+            if (n <= max_leaf && !force_median) return -1;
             if (n <= 4) return -1;
             const int mid = begin + n / 2;
             std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
@@ -189,8 +191,8 @@ struct Builder {
             }
         }
         const double leaf_cost = (double)n;
-        if (best_axis < 0 || (best_cost >= leaf_cost && n <= RT_MAX_LEAF)) {
-            if (n <= RT_MAX_LEAF) return -1;
+        if (best_axis < 0 || (best_cost >= leaf_cost && n <= max_leaf)) {
+            if (n <= max_leaf) return -1;
             const int mid = begin + n / 2;
             std::nth_element(items.begin() + begin, items.begin() + mid, items.begin() + end,
                              [axis](const Item &a, const Item &b) { return a.c[axis] < b.c[axis]; });
@@ -238,6 +240,7 @@ BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, f
     if (n <= 0) return res;
     const double ta = std::min(0.0, (double)time0), tb = std::max(0.0, (double)time1);
     Builder b;
+    if (const char *e = std::getenv("RTNW_BVH_MAX_LEAF")) b.max_leaf = std::max(1, std::min(RT_MAX_LEAF, std::atoi(e)));
     b.items.resize(n);
     for (int i = 0; i < n; i++) {
         Item &it = b.items[i];

@@ -14,14 +14,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 ap = argparse.ArgumentParser()
-ap.add_argument("libs", nargs="+")
+ap.add_argument("libs", nargs="+", help="LIB or LIB:VAR=VAL,VAR=VAL (extra environment)")
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--spp", type=int, default=1000)
 args = ap.parse_args()
 res = {lib: [] for lib in args.libs}
 for r in range(args.rounds):
     for lib in args.libs:
-        env = dict(os.environ, RTNW_LIB=os.path.abspath(lib))
+        path, _, extra = lib.partition(":")
+        env = dict(os.environ, RTNW_LIB=os.path.abspath(path))
+        for kv in filter(None, extra.split(",")):
+            k, _, v = kv.partition("=")
+            env[k] = v
         out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
                               "--spp", str(args.spp), "--no-cpu-baseline"], env=env, capture_output=True, text=True,
                              timeout=600)

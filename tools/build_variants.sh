@@ -1,17 +1,17 @@
 #!/bin/bash
-# tools/build_variants.sh N... — builds librt_hip.so variants with
-# __launch_bounds__(256, N) (N waves per SIMD) into variants/wN/ for A/B runs
-# (select one with RTNW_LIB=variants/wN/librt_hip.so).
+# tools/build_variants.sh NAME "DEFINES" ... — builds librt_hip.so variants of the
+# megakernel with extra -D flags into variants/NAME/ for A/B runs
+# (select one with RTNW_LIB=variants/NAME/librt_hip.so; tools/ab.py).
 set -e
 cd "$(dirname "$0")/../peter-shirley-ray-tracing-the-next-week_amd"
 make -s librt_hip.so
-for n in "$@"; do
-  mkdir -p ../variants/w$n
+while [ $# -ge 2 ]; do
+  name=$1; defs=$2; shift 2
+  mkdir -p ../variants/$name
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -Icsrc -Icsrc/host --offload-arch=gfx950 \
-      -munsafe-fp-atomics -DRT_WAVES_PER_SIMD=$n -c csrc/hip/rt_kernel.hip -o ../variants/w$n/rt_kernel.o
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../variants/w$n/librt_hip.so ../variants/w$n/rt_kernel.o \
+      -munsafe-fp-atomics $defs -c csrc/hip/rt_kernel.hip -o ../variants/$name/rt_kernel.o \
+      -Rpass-analysis=kernel-resource-usage 2> ../variants/$name/resource.txt
+  grep -A8 "ILb0ELb0" ../variants/$name/resource.txt | grep -E "VGPRs:|Scratch" | sed "s/.*remark: */$name: /"
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../variants/$name/librt_hip.so ../variants/$name/rt_kernel.o \
       build/capi.o build/bvh.o build/flatten.o build/rtnw.o -Wl,-rpath,/opt/rocm/lib
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -Icsrc -Icsrc/host --offload-arch=gfx950 \
-      -DRT_WAVES_PER_SIMD=$n -c csrc/hip/rt_kernel.hip -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 \
-      | grep -A8 "ILb0ELb0" | grep -E "VGPRs:|Scratch|Occupancy" | sed "s/^/w$n: /"
 done
