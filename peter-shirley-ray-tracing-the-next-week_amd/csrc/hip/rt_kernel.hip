@@ -363,9 +363,10 @@ constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
 // Minimum waves per SIMD the register allocation must allow (launch_bounds second
 // argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  Traversal is latency-bound, so
 // occupancy wins over the few spilled dwords: tools/ab.py, profiles/r01.
-// BVH traversal loop shape: 0 = node loop + leaf loop (while-while), 1 = one step per trip (if-if).
-#ifndef RT_TRAVERSAL_IFIF
-#define RT_TRAVERSAL_IFIF 0
+
+// Shade once this many lanes of a wave have their closest hit (see stage 3).
+#ifndef RT_READY_BATCH
+#define RT_READY_BATCH 48
 #endif
 
 #ifndef RT_WAVES_PER_SIMD
@@ -374,6 +375,9 @@ constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
 
 // kCount: visit counters (RT_FLAG_COUNT).  kProf: wave-level s_memtime stamps per
 // stage (RT_FLAG_PROFILE, a diagnostic build whose timing is never quoted).
+// Lane phases of the batched state machine below.
+enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
+
 template <bool kCount, bool kProf>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
@@ -384,17 +388,23 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
 
-    // lane state
+    // lane state: work item, path, traversal
     uint32_t item = 0xFFFFFFFFu;
     int s_cur = 0, s_end = 0;
     V3 part = mk(0, 0, 0);
-    bool path = false, finished = false;
+    int phase = PH_IDLE;
+    bool finished = false;
     Ray r;
     r.o = mk(0, 0, 0); r.d = mk(0, 0, 0); r.time = 0;
     V3 beta = mk(1, 1, 1);
     int depth = 0;
     Rng g; g.key = 0; g.mkey = 0; g.n = 0;
     uint32_t px = 0, py = 0;
+    uint32_t node = 0;
+    int sp = 0;
+    float best_t = RT_FLT_MAX;
+    int best_key = 0x7FFFFFFF;
+    uint32_t best_prim = 0xFFFFFFFFu;
 
     Counters cnt;
     uint64_t prof[4] = {0, 0, 0, 0};
@@ -406,15 +416,24 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             stamp = now;
         }
     };
-
+    // a new ray segment: closest-hit search from the root (hitable_list.h:20-32)
+    auto begin_segment = [&]() {
+        node = A.root;
+        sp = 0;
+        best_t = RT_FLT_MAX;
+        best_key = 0x7FFFFFFF;
+        best_prim = 0xFFFFFFFFu;
+        phase = A.has_bvh ? PH_TRAV : PH_READY;
+        if (kCount) cnt.segments++;
+    };
 
     for (;;) {
         // ---- 1. retire a finished work item, claim new ones ------------------
-        if (!path && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
+        if (phase == PH_IDLE && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
             A.slab[item] = make_float4(part.x, part.y, part.z, 0.f);
             item = 0xFFFFFFFFu;
         }
-        bool need = !path && !finished && item == 0xFFFFFFFFu;
+        bool need = phase == PH_IDLE && !finished && item == 0xFFFFFFFFu;
         uint64_t need_mask = __ballot(need);
         while (need_mask != 0ull && !exhausted) {
             if (pool_next == pool_end) {
@@ -446,8 +465,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         if (need) finished = true;
         if (__ballot(!finished) == 0ull) break;
 
-        // ---- 2. start a camera sample (main.cpp:305-308, camera.h:41-56) -----
-        if (!path && !finished) {
+        // ---- 2. start camera samples (main.cpp:305-308, camera.h:41-56) ------
+        if (phase == PH_IDLE && !finished) {
             int j = A.ny - 1 - (int)py;
             g.start(sample_key(A.seed, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
             float u = (float)((double)(int)px + g.next()) / (float)A.nx;
@@ -469,43 +488,27 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             r.time = time;
             beta = mk(1, 1, 1);
             depth = 0;
-            path = true;
             if (kCount) cnt.samples++;
+            begin_segment();
         }
-
         mark(0);
         if (kCount && first_active()) cnt.w_iters++;
-        if (!path) continue;   // finished lanes idle until the wave drains
 
-        // ---- 3. closest surface hit: BVH2, stack in LDS ------------------------
-        if (kCount) cnt.segments++;
-        float best_t = RT_FLT_MAX;
-        int best_key = 0x7FFFFFFF;
-        uint32_t best_prim = 0xFFFFFFFFu;
-        if (A.has_bvh) {
-            const float ix = 1.0f / r.d.x, iy = 1.0f / r.d.y, iz = 1.0f / r.d.z;
-            const float nox = -r.o.x * ix, noy = -r.o.y * iy, noz = -r.o.z * iz;
-            uint32_t node = A.root;
-            int sp = 0;
-#if RT_TRAVERSAL_IFIF
-            // if-if: every trip each lane does ONE step — a node step or one
-            // primitive test — so lanes in leaves and lanes in inner nodes share trips.
-            uint32_t lp = 0, le = 0;   // pending primitives of the open leaf
-            for (;;) {
-                if (node != RT_EMPTY_CHILD && (node & RT_LEAF_BIT)) {
-                    lp = RT_LEAF_FIRST(node);
-                    le = lp + RT_LEAF_COUNT(node);
-                    node = RT_EMPTY_CHILD;
-                }
-                if (lp < le) {
-                    int key, kind;
-                    float t = prim_t(A.prims, A.insts, lp, r, A.tmin, key, kind);
-                    if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                    if (t < best_t || (t == best_t && key < best_key)) {
-                        best_t = t; best_key = key; best_prim = lp;
-                    }
-                    ++lp;
-                } else {
+        // ---- 3. closest surface hit: BVH2 traversal rounds -------------------
+        // A round = descend to a leaf (or a dead end), test the leaf, pop.  The
+        // wave keeps running rounds for the lanes still searching until
+        // RT_READY_BATCH lanes have their hit, then shades that batch: a lane that
+        // finished early no longer holds the wave in traversal, and a lane still
+        // searching keeps its LDS stack and carries on in the next iteration.
+        for (;;) {
+            if (__ballot(phase == PH_TRAV) == 0ull) break;
+            if (__popcll(__ballot(phase == PH_READY)) >= RT_READY_BATCH) break;
+            if (phase == PH_TRAV) {
+                // the slab test needs no exact division: boxes are padded (bvh.cpp)
+                const float ix = __builtin_amdgcn_rcpf(r.d.x), iy = __builtin_amdgcn_rcpf(r.d.y),
+                            iz = __builtin_amdgcn_rcpf(r.d.z);
+                const float nox = -r.o.x * ix, noy = -r.o.y * iy, noz = -r.o.z * iz;
+                while (!(node & RT_LEAF_BIT)) {
                     if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
                     const float4 b0 = A.nodes[node * 4 + 0];
                     const float4 b1 = A.nodes[node * 4 + 1];
@@ -534,44 +537,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                         node = h0 ? c0 : (h1 ? c1 : RT_EMPTY_CHILD);
                     }
                 }
-                if (lp >= le && node == RT_EMPTY_CHILD) {
-                    if (sp == 0) break;
-                    --sp;
-                    node = stk[sp * 64];
-                }
-            }
-#else
-            for (;;) {
-                if (!(node & RT_LEAF_BIT)) {
-                    if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
-                    const float4 b0 = A.nodes[node * 4 + 0];
-                    const float4 b1 = A.nodes[node * 4 + 1];
-                    const float4 b2 = A.nodes[node * 4 + 2];
-                    const float4 cf = A.nodes[node * 4 + 3];
-                    const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-                    float a0 = __builtin_fmaf(b0.x, ix, nox), a1 = __builtin_fmaf(b0.y, ix, nox);
-                    float a2 = __builtin_fmaf(b0.z, iy, noy), a3 = __builtin_fmaf(b0.w, iy, noy);
-                    float a4 = __builtin_fmaf(b1.x, iz, noz), a5 = __builtin_fmaf(b1.y, iz, noz);
-                    float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), A.tmin));
-                    float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), best_t));
-                    float e0 = __builtin_fmaf(b1.z, ix, nox), e1 = __builtin_fmaf(b1.w, ix, nox);
-                    float e2 = __builtin_fmaf(b2.x, iy, noy), e3 = __builtin_fmaf(b2.y, iy, noy);
-                    float e4 = __builtin_fmaf(b2.z, iz, noz), e5 = __builtin_fmaf(b2.w, iz, noz);
-                    float tn1 = fmaxf(fmaxf(fminf(e0, e1), fminf(e2, e3)), fmaxf(fminf(e4, e5), A.tmin));
-                    float tf1 = fminf(fminf(fmaxf(e0, e1), fmaxf(e2, e3)), fminf(fmaxf(e4, e5), best_t));
-                    bool h0 = tn0 <= tf0 && c0 != RT_EMPTY_CHILD;
-                    bool h1 = tn1 <= tf1 && c1 != RT_EMPTY_CHILD;
-                    if (h0 && h1) {
-                        uint32_t nearc = c0, farc = c1;
-                        if (tn1 < tn0) { nearc = c1; farc = c0; }
-                        stk[sp * 64] = farc;
-                        ++sp;
-                        node = nearc;
-                        continue;
-                    }
-                    if (h0) { node = c0; continue; }
-                    if (h1) { node = c1; continue; }
-                } else {
+                if (node != RT_EMPTY_CHILD) {
                     const uint32_t first = RT_LEAF_FIRST(node), nleaf = RT_LEAF_COUNT(node);
                     for (uint32_t q = 0; q < nleaf; ++q) {
                         int key, kind;
@@ -582,14 +548,17 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                         }
                     }
                 }
-                if (sp == 0) break;
-                --sp;
-                node = stk[sp * 64];
+                if (sp == 0) {
+                    phase = PH_READY;
+                } else {
+                    --sp;
+                    node = stk[sp * 64];
+                }
             }
-#endif
         }
-
         mark(1);
+        if (phase != PH_READY) continue;   // still searching: carry on next iteration
+
         // ---- 4. media after the surfaces (constant_medium.h:26-50) -------------
         bool have = best_prim != 0xFFFFFFFFu;
         Hit hr;
@@ -736,6 +705,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                 r = ns;
                 ++depth;
                 terminate = false;
+                begin_segment();
             } else {
                 L = mul(beta, emitted);
             }
@@ -746,7 +716,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             if (!(L.z == L.z)) L.z = 0;
             part = add(part, L);
             ++s_cur;
-            path = false;
+            phase = PH_IDLE;
         }
         mark(3);
     }

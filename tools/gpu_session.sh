@@ -48,6 +48,7 @@ for step in "$@"; do
             run pmc_l2 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
             run pmc_sq 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     ab_trav) run ab_trav 1200 python3 tools/ab.py variants/ww/librt_hip.so variants/ifif/librt_hip.so variants/ww/librt_hip.so:RTNW_BVH_MAX_LEAF=4 variants/ifif/librt_hip.so:RTNW_BVH_MAX_LEAF=4 variants/ww/librt_hip.so:RTNW_BVH_MAX_LEAF=2 --rounds 2 ;;
+    ab_batch) run ab_batch 1500 python3 tools/ab.py variants/b32/librt_hip.so variants/b40/librt_hip.so variants/b48/librt_hip.so variants/b56/librt_hip.so variants/b64/librt_hip.so --rounds 2 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
