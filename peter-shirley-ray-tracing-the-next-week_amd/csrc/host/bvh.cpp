@@ -95,7 +95,9 @@ struct Item {
 };
 
 struct Builder {
-    int max_leaf = RT_MAX_LEAF;   // RTNW_BVH_MAX_LEAF overrides (<= RT_MAX_LEAF), for experiments
+    // SAH leaves hold at most 2 primitives: on final() that measured ~2% faster than 4 or 8
+    // (tools/ab.py); RTNW_BVH_MAX_LEAF overrides (<= RT_MAX_LEAF) for experiments.
+    int max_leaf = 2;
     std::vector<Item> items;
     std::vector<rt_dnode> nodes;
     std::vector<int> order;   // leaf order -> original prim index
