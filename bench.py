@@ -88,13 +88,16 @@ def cpu_baseline(budget_procs):
 
 
 def read_traffic(samples_per_launch):
-    """HBM bytes per launch from the committed PMC measurement (profiles/traffic.json,
-    written by tools/pmc_traffic.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3
-    passes of this workload, FETCH_SIZE doubled per the gfx950 correction), scaled to
-    this launch's sample count."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    """HBM bytes per launch from the latest committed PMC measurement
+    (profiles/r<NN>/traffic.json, written by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this workload, FETCH_SIZE doubled per
+    the gfx950 correction), scaled to this launch's sample count."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "traffic.json")))
+    if not found:
+        return None
     try:
-        with open(path) as f:
+        with open(found[-1]) as f:
             t = json.load(f)
         return t["hbm_bytes_per_sample"] * samples_per_launch
     except Exception:

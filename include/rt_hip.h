@@ -86,16 +86,23 @@ enum rt_texture_kind {
     RT_TEX_CONSTANT = 0, /* texture.h:16-27 color                    */
     RT_TEX_CHECKER = 1,  /* texture.h:30-45 even, odd (texture idx)  */
     RT_TEX_NOISE = 2,    /* texture.h:48-59 scale                    */
-    RT_TEX_IMAGE = 3     /* surface_texture.h:10-30 (not yet on device) */
+    RT_TEX_IMAGE = 3     /* surface_texture.h:10-30 image (index into images)      */
 };
 
 typedef struct rt_texture {
     int32_t kind;
-    int32_t even, odd;
-    float scale;
-    float color[3];
-    int32_t image;
+    int32_t even, odd;   /* checker children */
+    float scale;         /* noise */
+    float color[3];      /* constant */
+    int32_t image;       /* image: index into rt_scene_desc.images */
 } rt_texture;            /* 32 bytes */
+
+typedef struct rt_image {    /* texels of one image_texture (surface_texture.h:13) */
+    int64_t offset;          /* byte offset into rt_scene_desc.image_data */
+    int32_t nx, ny;          /* image size; texel (i, j) channel c is at 3*i + 3*nx*j + c
+                                (surface_texture.h:26-28 addresses with stride 3 whatever
+                                the file's channel count) */
+} rt_image;
 
 typedef struct rt_medium {   /* constant_medium.h:14-50 */
     int32_t boundary_first;  /* range in rt_scene_desc.boundary_prims */
@@ -118,6 +125,10 @@ typedef struct rt_scene_desc {
     const float *perlin_ranvec;   /* 256 x 3, perlin.h:82-87 */
     const int32_t *perlin_perm;   /* 3 x 256, perlin.h:99-111 */
     float time0, time1;           /* shutter span rays may carry (moving-sphere bounds) */
+    int32_t nimages;
+    const rt_image *images;
+    const uint8_t *image_data;    /* texel bytes of all images */
+    int64_t image_bytes;
 } rt_scene_desc;
 
 /* ------------------------------------------------------------------ camera */

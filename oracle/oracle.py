@@ -20,8 +20,9 @@ REF_BIN = os.path.join(HERE, "_ref", "ref_render")
 
 SCENES = {
     "random_scene": 0, "random_motion": 1, "cornell_box": 2, "cornell_smoke": 3,
-    "final": 4, "simple_light": 5, "two_spheres": 6, "test": 7,
+    "final": 4, "simple_light": 5, "two_spheres": 6, "test": 7, "earth": 8,
 }
+EARTH_PNG = os.path.join(os.path.dirname(HERE), "tests", "golden", "picture.png")   # main.cpp:93's asset
 CAMERAS = {"cornell": 0, "random": 1, "final_alt": 2}
 # Per-scene defaults, as the reference driver pairs them (main.cpp:254-291) plus
 # the chapter-1/3 sky background for the random scenes.
@@ -34,7 +35,62 @@ SCENE_DEFAULTS = {
     "simple_light": dict(camera="random", background="black", max_depth=50),
     "two_spheres": dict(camera="random", background="black", max_depth=50),
     "test": dict(camera="random", background="black", max_depth=50),
+    "earth": dict(camera="cornell", background="black", max_depth=50),
 }
+
+
+def png_rgba(path):
+    """Minimal 8-bit non-interlaced PNG decode (test-side; independent of the product's)."""
+    import struct
+    import zlib
+    d = open(path, "rb").read()
+    assert d[:8] == b"\x89PNG\r\n\x1a\n"
+    i, idat, w, h, ct = 8, b"", 0, 0, 0
+    while i < len(d):
+        n, = struct.unpack(">I", d[i:i + 4])
+        t = d[i + 4:i + 8]
+        if t == b"IHDR":
+            w, h, bd, ct = struct.unpack(">IIBB", d[i + 8:i + 18])
+            assert bd == 8
+        elif t == b"IDAT":
+            idat += d[i + 8:i + 8 + n]
+        i += 12 + n
+    ch = {0: 1, 2: 3, 4: 2, 6: 4}[ct]
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, w * ch + 1)
+    out = np.zeros((h, w * ch), np.int32)
+    for y in range(h):
+        f, row = raw[y, 0], raw[y, 1:].astype(np.int32)
+        up = out[y - 1] if y else np.zeros(w * ch, np.int32)
+        cur = np.zeros(w * ch, np.int32)
+        for x in range(w * ch):
+            a = cur[x - ch] if x >= ch else 0
+            b = up[x]
+            c = up[x - ch] if x >= ch else 0
+            if f == 0: v = row[x]
+            elif f == 1: v = row[x] + a
+            elif f == 2: v = row[x] + b
+            elif f == 3: v = row[x] + ((a + b) >> 1)
+            else:
+                p = a + b - c
+                pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
+                v = row[x] + (a if pa <= pb and pa <= pc else (b if pb <= pc else c))
+            cur[x] = v & 255
+        out[y] = cur
+    return out.astype(np.uint8).reshape(h, w, ch)
+
+
+_image_loaded = False
+
+
+def load_earth_image(path=None):
+    """Hands earth()'s texels to the oracle (done once per process)."""
+    global _image_loaded
+    if _image_loaded:
+        return
+    img = np.ascontiguousarray(png_rgba(path or EARTH_PNG))
+    h, w, ch = img.shape
+    lib().oracle_set_image(img.ctypes.data, w, h, ch)
+    _image_loaded = True
 
 
 class OracleParams(ctypes.Structure):
@@ -73,6 +129,7 @@ def lib():
         L.oracle_medium_draw.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
         L.oracle_medium_draw.restype = ctypes.c_double
         L.oracle_scene_dump.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_long]
+        L.oracle_set_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_scene_dump.restype = ctypes.c_long
         _lib = L
     return _lib
@@ -105,6 +162,8 @@ class RenderSpec:
 
 def render(spec: RenderSpec):
     """Returns (mean float32 array [h, w, 3], stats dict)."""
+    if spec.scene == "earth":
+        load_earth_image()
     depth, bg, cam = spec.resolved()
     x0, y0, w, h = spec.rect if spec.rect else (0, 0, spec.nx, spec.ny)
     p = OracleParams(scene=SCENES[spec.scene], nx=spec.nx, ny=spec.ny, ns=spec.ns, max_depth=depth,
@@ -172,6 +231,8 @@ def medium_draw(seed: int, pixel: int, sample: int, bounce: int, medium: int) ->
 
 
 def scene_dump(scene: str) -> str:
+    if scene == "earth":
+        load_earth_image()
     n = lib().oracle_scene_dump(SCENES[scene], None, 0)
     buf = ctypes.create_string_buffer(n)
     lib().oracle_scene_dump(SCENES[scene], buf, n)
@@ -190,7 +251,8 @@ def ref_render(spec: RenderSpec, workdir: str, rows: tuple | None = None, timing
     ppm = os.path.join(workdir, "ref.ppm")
     cmd = [REF_BIN, "--scene", spec.scene, "--nx", str(spec.nx), "--ny", str(spec.ny), "--ns", str(spec.ns),
            "--depth", str(depth), "--bg", bg, "--cam", cam, "--tmin", repr(spec.tmin),
-           "--rng", spec.rng, "--seed", str(spec.seed), "--fb", fb, "--ppm", ppm]
+           "--rng", spec.rng, "--seed", str(spec.seed), "--fb", fb, "--ppm", ppm,
+           "--assets", os.path.dirname(EARTH_PNG)]
     if rows:
         cmd += ["--rows", f"{rows[0]}:{rows[1]}"]
     if timing:
@@ -209,7 +271,8 @@ def ref_render(spec: RenderSpec, workdir: str, rows: tuple | None = None, timing
 
 def ref_dump(scene: str, workdir: str) -> str:
     path = os.path.join(workdir, f"dump_{scene}.txt")
-    subprocess.run([REF_BIN, "--scene", scene, "--nx", "1", "--ny", "1", "--ns", "1", "--dump", path],
+    subprocess.run([REF_BIN, "--scene", scene, "--nx", "1", "--ny", "1", "--ns", "1", "--dump", path,
+                    "--assets", os.path.dirname(EARTH_PNG)],
                    capture_output=True, check=True)
     with open(path) as f:
         return f.read()

@@ -29,6 +29,7 @@
 #include <chrono>
 #include <string>
 #include <vector>
+#include <unistd.h>
 
 
 
@@ -183,7 +184,13 @@ static void dump_tex(const texture *t) {
     if (auto *c = dynamic_cast<const constant_texture *>(t)) { fprintf(g_dump, "(const %a %a %a)", c->color[0], c->color[1], c->color[2]); return; }
     if (auto *k = dynamic_cast<const checker_texture *>(t)) { fprintf(g_dump, "(checker even="); dump_tex(k->even); fprintf(g_dump, " odd="); dump_tex(k->odd); fprintf(g_dump, ")"); return; }
     if (auto *n = dynamic_cast<const noise_texture *>(t)) { fprintf(g_dump, "(noise %a)", n->scale); return; }
-    fprintf(g_dump, "(image)");
+    if (auto *im = dynamic_cast<const image_texture *>(t)) {
+        uint32_t h = 2166136261u;   // FNV-1a over the texels value() can address (stride 3)
+        for (long b = 0; b < 3L * im->nx * im->ny; b++) h = (h ^ im->data[b]) * 16777619u;
+        fprintf(g_dump, "(image %d %d %08x)", im->nx, im->ny, h);
+        return;
+    }
+    fprintf(g_dump, "(unknown texture)");
 }
 static void dump_mat(const material *m) {
     fprintf(g_dump, " mat%d=", ptr_id(g_mats, m));
@@ -232,7 +239,7 @@ static void usage() {
 }
 
 int main(int argc, char **argv) {
-    std::string scene = "final", cam_name = "", bg = "", rng = "canonical", ppm, fb, dump, perlin_out;
+    std::string scene = "final", cam_name = "", bg = "", rng = "canonical", ppm, fb, dump, perlin_out, assets;
     int nx = 40, ny = 40, ns = 4, depth = -1, j_lo = 0, j_hi = -1; bool timing = false;
     double tmin = 0.001; uint64_t seed = 0;
     for (int a = 1; a < argc; a++) {
@@ -254,6 +261,7 @@ int main(int argc, char **argv) {
         else if (k == "--dump") dump = val();
         else if (k == "--perlin") perlin_out = val();
         else if (k == "--time") timing = true;
+        else if (k == "--assets") assets = val();
         else usage();
     }
     if (j_hi < 0) j_hi = ny;
@@ -280,6 +288,10 @@ int main(int argc, char **argv) {
     else if (scene == "simple_light") { world = simple_light(); cam_default = "random"; }
     else if (scene == "two_spheres") { world = two_spheres(); cam_default = "random"; }
     else if (scene == "test") { world = test(); cam_default = "random"; }
+    else if (scene == "earth") {   // stbi_load("picture.png") reads the working directory (main.cpp:93)
+        if (!assets.empty() && chdir(assets.c_str()) != 0) { perror("chdir"); return 2; }
+        world = earth();
+    }
     else usage();
     std::cout.rdbuf(saved);
 

@@ -154,8 +154,11 @@ static float perlin_turb(v3 p) {                                         /* perl
 }
 
 /* -------------------------------------------------------------- textures */
-enum { TX_CONST, TX_CHECKER, TX_NOISE };
-typedef struct tex_s { int kind; v3 color; const struct tex_s *even, *odd; float scale; } tex_t;
+enum { TX_CONST, TX_CHECKER, TX_NOISE, TX_IMAGE };
+typedef struct tex_s {
+    int kind; v3 color; const struct tex_s *even, *odd; float scale;
+    const unsigned char *data; int nx, ny;   /* image_texture, surface_texture.h:13-16 */
+} tex_t;
 
 static v3 tex_value(const tex_t *t, float u, float v, v3 p) {
     for (;;) {
@@ -164,6 +167,18 @@ static v3 tex_value(const tex_t *t, float u, float v, v3 p) {
             float sines = sinf(10 * p.e[0]) * sinf(10 * p.e[1]) * sinf(10 * p.e[2]);
             t = (sines < 0) ? t->odd : t->even;
             continue;
+        }
+        if (t->kind == TX_IMAGE) {                                            /* surface_texture.h:19-30 */
+            int i = (int)((1 - u) * t->nx);
+            int j = (int)((double)((1 - v) * t->ny) - 0.001);
+            if (i < 0) i = 0;
+            if (j < 0) j = 0;
+            if (i > t->nx - 1) i = t->nx - 1;
+            if (j > t->ny - 1) j = t->ny - 1;
+            float r = (float)((int)t->data[3 * i + 3 * t->nx * j] / 255.0);
+            float g = (float)((int)t->data[3 * i + 3 * t->nx * j + 1] / 255.0);
+            float b = (float)((int)t->data[3 * i + 3 * t->nx * j + 2] / 255.0);
+            return V(r, g, b);
         }
         /* noise_texture, texture.h:52-56 */
         float s = 1 + sinf(t->scale * p.e[0] + 5 * perlin_turb(vscale(t->scale, p)));
@@ -615,6 +630,27 @@ static obj_t *build_two_spheres(scene_t *s) {                             /* mai
     return o_list(s, list, 2);
 }
 
+static unsigned char *g_image;
+static int g_image_nx, g_image_ny;
+
+void oracle_set_image(const uint8_t *data, int nx, int ny, int nn) {
+    free(g_image);
+    g_image = malloc((size_t)nx * ny * nn);
+    memcpy(g_image, data, (size_t)nx * ny * nn);
+    g_image_nx = nx;
+    g_image_ny = ny;
+}
+
+static obj_t *build_earth(scene_t *s) {                                   /* main.cpp:87-97 */
+    obj_t **list = o_array(s, 2);
+    mat_t *light = m_light(s, t_const(s, 7, 7, 7));
+    list[0] = o_rect(s, OB_XZ, 63, 483, 55, 482, 554, light);
+    tex_t *t = arena_alloc(s, sizeof *t);
+    t->kind = TX_IMAGE; t->data = g_image; t->nx = g_image_nx; t->ny = g_image_ny;
+    list[1] = o_sphere(s, V(360, 250, 150), 100, m_lambert(s, t));
+    return o_list(s, list, 2);
+}
+
 static obj_t *build_test(scene_t *s) {                                    /* main.cpp:135-145 */
     tex_t *pertext = t_noise(s, 4);
     tex_t *checker = t_checker(s, t_const(s, 0.2, 0.3, 0.1), t_const(s, 0.9, 0.9, 0.9));
@@ -649,6 +685,7 @@ static int scene_build(scene_t *s, int which, rng_t *g_after) {
     case ORACLE_SCENE_SIMPLE_LIGHT: s->world = build_simple_light(s); break;
     case ORACLE_SCENE_TWO_SPHERES: s->world = build_two_spheres(s); break;
     case ORACLE_SCENE_TEST: s->world = build_test(s); break;
+    case ORACLE_SCENE_EARTH: if (!g_image) return -1; s->world = build_earth(s); break;
     default: return -1;
     }
     collect_media(s, s->world);
@@ -909,7 +946,10 @@ static int dump_id(dump_t *d, const void *p) {
 static void dump_tex(dump_t *d, const tex_t *t) {
     if (t->kind == TX_CONST) { dputs(d, "(const %a %a %a)", t->color.e[0], t->color.e[1], t->color.e[2]); return; }
     if (t->kind == TX_CHECKER) { dputs(d, "(checker even="); dump_tex(d, t->even); dputs(d, " odd="); dump_tex(d, t->odd); dputs(d, ")"); return; }
-    dputs(d, "(noise %a)", t->scale);
+    if (t->kind == TX_NOISE) { dputs(d, "(noise %a)", t->scale); return; }
+    uint32_t h = 2166136261u;   /* FNV-1a over the addressable texels */
+    for (long b = 0; b < 3L * t->nx * t->ny; b++) h = (h ^ t->data[b]) * 16777619u;
+    dputs(d, "(image %d %d %08x)", t->nx, t->ny, h);
 }
 static void dump_mat(dump_t *d, const mat_t *m) {
     dputs(d, " mat%d=", dump_id(d, m));

@@ -17,6 +17,7 @@ struct RtKernelArgs {
     const float4 *insts;    // 7 x float4 per instance chain
     const float4 *ranvec;   // 256 Perlin gradients (w unused)
     const int *perm;        // 3 x 256 Perlin permutations
+    const uint8_t *texels;  // image_texture bytes
     uint32_t root;
     int has_bvh;
     int nmedia;

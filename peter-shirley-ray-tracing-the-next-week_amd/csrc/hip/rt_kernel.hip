@@ -212,11 +212,22 @@ __device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, ui
     return t;
 }
 
-struct Hit { V3 p, n; int mat; };
+struct Hit { V3 p, n; float u, v; int mat; };
+
+// get_sphere_uv (hitable.h:14-19): float atan2/asin, then the double M_PI arithmetic.
+__device__ __forceinline__ void sphere_uv(V3 p, float &u, float &v) {
+    const float phi = atan2f(p.z, p.x);
+    const float theta = asinf(p.y);
+    u = (float)(1 - ((double)phi + 3.14159265358979323846) / (2 * 3.14159265358979323846));
+    v = (float)(((double)theta + 3.14159265358979323846 / 2) / 3.14159265358979323846);
+}
 
 // Rebuilds the reference's hit_record for the winning primitive (sphere.h:34-38,
 // 103-106; aarect.h:58-63; hitable.h:43-45, 69, 137-145).
-__device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float t) {
+// (u, v) is computed only for materials whose texture reads it (an image texture):
+// every other texture ignores it (texture.h:22-56).
+__device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts, const float4 *mats, uint32_t idx,
+                                           const Ray &r0, float t) {
     const float4 g0 = P[idx * 4 + 0];
     const float4 g1 = P[idx * 4 + 1];
     const float4 g2 = P[idx * 4 + 2];
@@ -236,9 +247,24 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
         int axis = rect_axis(kind);
         h.n = mk(axis == 0 ? 1.f : 0.f, axis == 1 ? 1.f : 0.f, axis == 2 ? 1.f : 0.f);
     }
+    h.u = 0.f;
+    h.v = 0.f;
+    h.mat = fbits(mm.y);
+    if (fbits(mats[h.mat * 2 + 1].w) & 1) {
+        if (kind == RT_PRIM_SPHERE) {
+            sphere_uv(divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w), h.u, h.v);   // sphere.h:36
+        } else if (kind != RT_PRIM_MOVING_SPHERE) {                          // aarect.h:54-59
+            float oi, di, oj, dj;
+            if (kind == RT_PRIM_XY_RECT) { oi = r.o.x; di = r.d.x; oj = r.o.y; dj = r.d.y; }
+            else if (kind == RT_PRIM_XZ_RECT) { oi = r.o.x; di = r.d.x; oj = r.o.z; dj = r.d.z; }
+            else { oi = r.o.y; di = r.d.y; oj = r.o.z; dj = r.d.z; }
+            const float a = oi + t * di, b = oj + t * dj;
+            h.u = (a - g0.x) / (g0.y - g0.x);
+            h.v = (b - g0.z) / (g0.w - g0.z);
+        }
+    }
     if (flip) h.n = neg(h.n);
     if (inst >= 0) to_world(insts, inst, h.p, h.n);
-    h.mat = fbits(mm.y);
     return h;
 }
 
@@ -318,7 +344,7 @@ __device__ float perlin_turb(const float4 *ranvec, const int *perm, V3 p) {   //
 }
 
 template <bool kCount>
-__device__ V3 tex_value(const RtKernelArgs &A, int ti, V3 p, Counters &cnt) {   // texture.h:16-59
+__device__ V3 tex_value(const RtKernelArgs &A, int ti, float u, float v, V3 p, Counters &cnt) {   // texture.h:16-59
     for (int guard = 0; guard < RT_MAX_CHECKER_DEPTH; ++guard) {
         const float4 t0 = A.texs[ti * 2 + 0];
         const float4 t1 = A.texs[ti * 2 + 1];
@@ -328,6 +354,20 @@ __device__ V3 tex_value(const RtKernelArgs &A, int ti, V3 p, Counters &cnt) {   
             float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
             ti = (sines < 0) ? fbits(t0.z) : fbits(t0.y);
             continue;
+        }
+        if (kind == RT_TEX_IMAGE) {   // surface_texture.h:19-30 (stride 3 as the reference addresses it)
+            const int nx = fbits(t0.y), ny = fbits(t0.z);
+            const uint8_t *data = A.texels + fbits(t0.w);
+            int i = (int)((1 - u) * nx);
+            int j = (int)((double)((1 - v) * ny) - 0.001);
+            if (i < 0) i = 0;
+            if (j < 0) j = 0;
+            if (i > nx - 1) i = nx - 1;
+            if (j > ny - 1) j = ny - 1;
+            const float r = (float)((int)data[3 * i + 3 * nx * j] / 255.0);
+            const float gg = (float)((int)data[3 * i + 3 * nx * j + 1] / 255.0);
+            const float b = (float)((int)data[3 * i + 3 * nx * j + 2] / 255.0);
+            return mk(r, gg, b);
         }
         // RT_TEX_NOISE
         if (kCount) cnt.noise++;
@@ -562,7 +602,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         // ---- 4. media after the surfaces (constant_medium.h:26-50) -------------
         bool have = best_prim != 0xFFFFFFFFu;
         Hit hr;
-        if (have) hr = prim_record(A.prims, A.insts, best_prim, r, best_t);
+        if (have) hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
         for (int k = 0; k < A.nmedia; ++k) {
             if (kCount) cnt.media++;
             const int4 md = A.media[k];
@@ -607,6 +647,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                 have = true;
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);
+                hr.u = 0.f;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
+                hr.v = 0.f;
                 hr.mat = md.w;
             }
         }
@@ -638,7 +680,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             const bool textured = kind == RT_MAT_DIFFUSE_LIGHT ||
                                   (live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC));
             V3 tv = mk(0, 0, 0);
-            if (textured) tv = tex_value<kCount>(A, tex, hr.p, cnt);          // texture.h / perlin.h
+            if (textured) tv = tex_value<kCount>(A, tex, hr.u, hr.v, hr.p, cnt);          // texture.h / perlin.h
             const bool wants_sphere = live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_METAL ||
                                                kind == RT_MAT_ISOTROPIC);
             V3 rius = mk(0, 0, 0);

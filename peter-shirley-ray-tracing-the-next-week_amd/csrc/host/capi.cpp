@@ -95,7 +95,7 @@ struct rt_scene {
     hipStream_t own_stream = nullptr;
     // scene in HBM
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
-         *insts = nullptr, *ranvec = nullptr, *perm = nullptr;
+         *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr;
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0;
     bool has_moving = false;
@@ -155,6 +155,8 @@ static int validate_desc(const rt_scene_desc *d) {
         return fail(RT_ERR_INVALID, "negative count in scene descriptor");
     if (d->nprims > (1 << 24) - 1 || d->nboundary > (1 << 24) - 1) return fail(RT_ERR_INVALID, "too many primitives");
     if (!d->perlin_ranvec || !d->perlin_perm) return fail(RT_ERR_INVALID, "missing Perlin tables");
+    if (d->nimages < 0 || d->image_bytes < 0 || (d->nimages > 0 && (!d->images || !d->image_data)))
+        return fail(RT_ERR_INVALID, "bad image arrays");
     auto check_prim = [&](const rt_prim &p) -> int {
         if (p.kind < RT_PRIM_SPHERE || p.kind > RT_PRIM_YZ_RECT) return fail(RT_ERR_INVALID, "bad primitive kind");
         if (p.material < 0 || p.material >= d->nmaterials) return fail(RT_ERR_INVALID, "primitive material out of range");
@@ -179,8 +181,14 @@ static int validate_desc(const rt_scene_desc *d) {
     }
     for (int i = 0; i < d->ntextures; i++) {
         const rt_texture &t = d->textures[i];
-        if (t.kind == RT_TEX_IMAGE) return fail(RT_ERR_UNSUPPORTED, "image_texture is not supported on the device yet");
         if (t.kind < RT_TEX_CONSTANT || t.kind > RT_TEX_IMAGE) return fail(RT_ERR_INVALID, "bad texture kind");
+        if (t.kind == RT_TEX_IMAGE) {
+            if (t.image < 0 || t.image >= d->nimages) return fail(RT_ERR_INVALID, "image texture index out of range");
+            const rt_image &im = d->images[t.image];
+            if (im.nx <= 0 || im.ny <= 0 || im.offset < 0 ||
+                im.offset + (int64_t)3 * im.nx * im.ny > d->image_bytes || im.offset > 0x7FFFFFFF)
+                return fail(RT_ERR_INVALID, "image texels out of range");
+        }
         if (t.kind == RT_TEX_CHECKER) {
             if (t.even < 0 || t.even >= d->ntextures || t.odd < 0 || t.odd >= d->ntextures)
                 return fail(RT_ERR_INVALID, "checker child out of range");
@@ -212,7 +220,7 @@ static int validate_desc(const rt_scene_desc *d) {
 void rt_scene_destroy(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    for (void *p : {s->nodes, s->prims, s->bprims, s->media, s->mats, s->texs, s->insts, s->ranvec, s->perm, s->job_xy,
+    for (void *p : {s->nodes, s->prims, s->bprims, s->media, s->mats, s->texs, s->insts, s->ranvec, s->perm, s->texels, s->job_xy,
                     s->job_out, s->slab, s->counter, s->stats, s->host_out})
         if (p) (void)hipFree(p);
     for (auto &e : s->ev) if (e) (void)hipEventDestroy(e);
@@ -253,6 +261,18 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         bprims[i] = to_dprim(d->boundary_prims[i], i);
         s->has_moving |= d->boundary_prims[i].kind == RT_PRIM_MOVING_SPHERE;
     }
+    // a material whose texture tree reaches an image needs the hit's (u, v)
+    auto reads_uv = [&](int t) {
+        std::vector<int> st{t};
+        while (!st.empty()) {
+            const int x = st.back();
+            st.pop_back();
+            if (x < 0) continue;
+            if (d->textures[x].kind == RT_TEX_IMAGE) return true;
+            if (d->textures[x].kind == RT_TEX_CHECKER) { st.push_back(d->textures[x].even); st.push_back(d->textures[x].odd); }
+        }
+        return false;
+    };
     std::vector<rt_dmaterial> mats(d->nmaterials);
     for (int i = 0; i < d->nmaterials; i++) {
         const rt_material &m = d->materials[i];
@@ -262,7 +282,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         o.fuzz = m.fuzz;
         o.ref_idx = m.ref_idx;
         for (int k = 0; k < 3; k++) o.albedo[k] = m.albedo[k];
-        o.flags = 0;
+        o.flags = (m.texture >= 0 && reads_uv(m.texture)) ? 1 : 0;
     }
     std::vector<rt_dtexture> texs(d->ntextures);
     for (int i = 0; i < d->ntextures; i++) {
@@ -273,6 +293,12 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         o.odd = t.odd;
         o.scale = t.scale;
         for (int k = 0; k < 3; k++) o.color[k] = t.color[k];
+        if (t.kind == RT_TEX_IMAGE) {   // (kind, nx, ny, byte offset)
+            const rt_image &im = d->images[t.image];
+            o.even = im.nx;
+            o.odd = im.ny;
+            o.scale = fbits((int)im.offset);
+        }
     }
     std::vector<rt_dinstance> insts(d->ninstances);
     for (int i = 0; i < d->ninstances; i++) {
@@ -294,12 +320,14 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     std::vector<float> ranvec(256 * 4, 0.0f);
     for (int i = 0; i < 256; i++) for (int k = 0; k < 3; k++) ranvec[4 * i + k] = d->perlin_ranvec[3 * i + k];
     std::vector<int32_t> perm(d->perlin_perm, d->perlin_perm + 768);
+    std::vector<uint8_t> texels(d->image_data, d->image_data + (d->nimages > 0 ? d->image_bytes : 0));
     for (int v : perm) if (v < 0 || v > 255) return cleanup(fail(RT_ERR_INVALID, "Perlin permutation entry out of range"));
 
     int rc;
     if ((rc = upload(&s->nodes, bvh.nodes)) || (rc = upload(&s->prims, prims)) || (rc = upload(&s->bprims, bprims)) ||
         (rc = upload(&s->media, media)) || (rc = upload(&s->mats, mats)) || (rc = upload(&s->texs, texs)) ||
-        (rc = upload(&s->insts, insts)) || (rc = upload(&s->ranvec, ranvec)) || (rc = upload(&s->perm, perm)))
+        (rc = upload(&s->insts, insts)) || (rc = upload(&s->ranvec, ranvec)) || (rc = upload(&s->perm, perm)) ||
+        (rc = upload(&s->texels, texels)))
         return cleanup(rc);
     s->root = bvh.root;
     s->has_bvh = d->nprims > 0;
@@ -400,6 +428,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.insts = (const float4 *)s->insts;
     a.ranvec = (const float4 *)s->ranvec;
     a.perm = (const int *)s->perm;
+    a.texels = (const uint8_t *)s->texels;
     a.root = s->root;
     a.has_bvh = s->has_bvh;
     a.nmedia = s->nmedia;

@@ -47,3 +47,4 @@ using rtnw::translate;
 using rtnw::rotate_y;
 using rtnw::constant_medium;
 using rtnw::bvh_node;
+using rtnw::stbi_load;

@@ -109,7 +109,16 @@ int image_texture::flatten(flat_ctx &cx) const {
     rt_texture t{};
     t.kind = RT_TEX_IMAGE;
     t.even = t.odd = -1;
-    t.image = -1;
+    // the texels value() can address: 3 bytes per texel (surface_texture.h:26-28)
+    rt_image im{};
+    im.offset = (int64_t)cx.out->image_data.size();
+    im.nx = nx;
+    im.ny = ny;
+    const size_t n = data ? (size_t)3 * (size_t)nx * (size_t)ny : 0;
+    if (!data || nx <= 0 || ny <= 0) throw std::runtime_error("image_texture without pixels (stbi_load failed?)");
+    cx.out->image_data.insert(cx.out->image_data.end(), data, data + n);
+    cx.out->images.push_back(im);
+    t.image = (int32_t)cx.out->images.size() - 1;
     return cx.add_texture(t);
 }
 
@@ -207,6 +216,10 @@ std::unique_ptr<flat_scene> flatten_world(const hitable *world, float time0, flo
     d.perlin_perm = fs->perm.data();
     d.time0 = time0;
     d.time1 = time1;
+    d.nimages = (int32_t)fs->images.size();
+    d.images = fs->images.data();
+    d.image_data = fs->image_data.data();
+    d.image_bytes = (int64_t)fs->image_data.size();
     return fs;
 }
 
@@ -231,7 +244,12 @@ struct dumper {
         if (x.kind == RT_TEX_CONSTANT) put("(const %a %a %a)", x.color[0], x.color[1], x.color[2]);
         else if (x.kind == RT_TEX_CHECKER) { put("(checker even="); tex(x.even); put(" odd="); tex(x.odd); put(")"); }
         else if (x.kind == RT_TEX_NOISE) put("(noise %a)", x.scale);
-        else put("(image)");
+        else {
+            const rt_image &im = d->images[x.image];
+            uint32_t h = 2166136261u;   // FNV-1a over the addressable texels
+            for (int64_t b = 0; b < (int64_t)3 * im.nx * im.ny; b++) h = (h ^ d->image_data[im.offset + b]) * 16777619u;
+            put("(image %d %d %08x)", im.nx, im.ny, h);
+        }
     }
     void mat(int m) {
         auto it = ids.find(m);

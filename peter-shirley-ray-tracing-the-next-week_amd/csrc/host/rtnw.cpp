@@ -380,6 +380,17 @@ hitable *final_scene() {   // main.cpp:190-230
     return new hitable_list(list, l);
 }
 
+hitable *earth(const char *png_path) {   // main.cpp:87-97
+    hitable **list = new hitable *[2];
+    material *light = new diffuse_light(new constant_texture(vec3(7, 7, 7)));
+    list[0] = new xz_rect(63, 483, 55, 482, 554, light);
+    int nx, ny, nn;
+    unsigned char *tex_data = stbi_load(png_path, &nx, &ny, &nn, 0);
+    material *mat = new lambertian(new image_texture(tex_data, nx, ny));
+    list[1] = new sphere(vec3(360, 250, 150), 100, mat);
+    return new hitable_list(list, 2);
+}
+
 hitable *build_named_scene(const std::string &name, float *time0, float *time1) {
     reset_reference_rng();
     *time0 = 0.0f;
@@ -392,6 +403,10 @@ hitable *build_named_scene(const std::string &name, float *time0, float *time1) 
     if (name == "simple_light") return simple_light();
     if (name == "two_spheres") return two_spheres();
     if (name == "test") return test_scene();
+    if (name == "earth") {
+        const char *png = std::getenv("RTNW_EARTH_PNG");
+        return earth(png ? png : "picture.png");
+    }
     return nullptr;
 }
 

@@ -162,8 +162,13 @@ public:
     int nx, ny;
     image_texture() {}
     image_texture(unsigned char *pixels, int A, int B) : data(pixels), nx(A), ny(B) {}
-    int flatten(flat_ctx &cx) const override;   // not yet supported on the device
+    int flatten(flat_ctx &cx) const override;
 };
+
+// PNG reader standing in for the vendored stb_image the reference calls (main.cpp:93):
+// same signature and result (channels as stored when req_comp == 0), 8-bit PNG only.
+unsigned char *stbi_load(const char *filename, int *x, int *y, int *comp, int req_comp);
+unsigned char *png_decode(const unsigned char *buf, size_t len, int *x, int *y, int *comp, std::string *err);
 
 // ----------------------------------------------------------------- materials
 class material {
@@ -375,6 +380,8 @@ struct flat_scene {
     std::vector<rt_instance> instances;
     std::vector<float> ranvec;      // 768
     std::vector<int32_t> perm;      // 768
+    std::vector<rt_image> images;
+    std::vector<uint8_t> image_data;
     rt_scene_desc desc{};           // points into the vectors above
 };
 // Flattens `world`; time0/time1 is the shutter span rays may carry.
@@ -395,6 +402,9 @@ hitable *test_scene();           // main.cpp:135-145 (`test`)
 hitable *cornell_box();          // main.cpp:148-166
 hitable *cornell_smoke();        // main.cpp:169-188
 hitable *final_scene();          // main.cpp:190-230 (`final`)
+// main.cpp:87-97 (`earth`); the reference reads "picture.png" from the working
+// directory; build_named_scene("earth") reads $RTNW_EARTH_PNG if set.
+hitable *earth(const char *png_path = "picture.png");
 
 // Builds a named scene as a fresh reference process would (reset_reference_rng first).
 hitable *build_named_scene(const std::string &name, float *time0, float *time1);

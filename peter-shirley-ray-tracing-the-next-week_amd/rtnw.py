@@ -195,6 +195,7 @@ SCENE_DEFAULTS = {   # per-scene camera / background / depth pairing (SURVEY §8
     "simple_light": ("random", RT_BG_BLACK, 50),
     "two_spheres": ("random", RT_BG_BLACK, 50),
     "test": ("random", RT_BG_BLACK, 50),
+    "earth": ("cornell", RT_BG_BLACK, 50),
 }
 
 
@@ -211,7 +212,11 @@ class SceneDesc:
         self.ptr = ptr
 
     @classmethod
-    def builtin(cls, name: str) -> "SceneDesc":
+    def builtin(cls, name: str, earth_png: str | None = None) -> "SceneDesc":
+        """earth() reads its texture like the reference (main.cpp:93): "picture.png" in
+        the working directory, or earth_png / $RTNW_EARTH_PNG."""
+        if name == "earth" and earth_png:
+            os.environ["RTNW_EARTH_PNG"] = earth_png
         p = ctypes.POINTER(RtSceneDesc)()
         _check(lib().rt_builtin_scene_desc(name.encode(), ctypes.byref(p)))
         return cls(p)
@@ -247,8 +252,8 @@ class Scene:
         _check(lib().rt_scene_create(desc.ptr, device, ctypes.byref(self.handle)))
 
     @classmethod
-    def builtin(cls, name: str, device: int = 0) -> "Scene":
-        return cls(SceneDesc.builtin(name), device)
+    def builtin(cls, name: str, device: int = 0, earth_png: str | None = None) -> "Scene":
+        return cls(SceneDesc.builtin(name, earth_png), device)
 
     def render_tile(self, cam: Camera, params: RtRenderParams, x0, y0, w, h, stats: bool = False):
         out = np.zeros((h, w, 3), dtype=np.float32)

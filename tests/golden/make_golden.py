@@ -29,13 +29,14 @@ import oracle as O  # noqa: E402
 CANONICAL = [
     ("final", 40, 40, 4), ("final", 100, 100, 10), ("random_scene", 200, 100, 10), ("cornell_box", 40, 40, 8),
     ("cornell_smoke", 32, 32, 4), ("random_motion", 40, 20, 4), ("simple_light", 40, 20, 4),
-    ("two_spheres", 20, 20, 4), ("test", 20, 20, 4),
+    ("two_spheres", 20, 20, 4), ("test", 20, 20, 4), ("earth", 40, 40, 8),
 ]
 # counter-RNG reference framebuffers: (name, scene, nx, ny, ns, seed)
 COUNTER = [
     ("c1_random", "random_scene", 40, 20, 4, 1), ("c2_cornell", "cornell_box", 24, 24, 8, 2),
     ("c3_motion", "random_motion", 40, 20, 4, 3), ("c4_final", "final", 24, 24, 8, 4),
     ("smoke", "cornell_smoke", 24, 24, 8, 5), ("simple_light", "simple_light", 32, 16, 4, 6),
+    ("earth", "earth", 32, 32, 8, 7),
 ]
 
 

@@ -18,10 +18,11 @@ import tempfile
 
 import pytest
 
+import oracle as O
 import rtnw
 
 REF_MAIN = "/root/reference/Peter-Shirley-Project Code/main.cpp"
-BUILDERS = ["random_scene", "two_spheres", "simple_light", "test", "cornell_box", "cornell_smoke", "final"]
+BUILDERS = ["random_scene", "earth", "two_spheres", "simple_light", "test", "cornell_box", "cornell_smoke", "final"]
 CLANG = "/opt/rocm/lib/llvm/bin/clang++"
 
 pytestmark = pytest.mark.skipif(not os.path.exists(REF_MAIN), reason="reference tree not present")
@@ -62,7 +63,8 @@ def test_reference_builders_compile_and_match(golden):
                     "-I", os.path.join(os.path.dirname(pkg), "include"), cpp, "-o", exe,
                     "-L", pkg, "-lrt_hip", f"-Wl,-rpath,{pkg}"], check=True)
     dump = os.path.join(work, "dump.txt")
-    subprocess.run([exe, dump], check=True)
+    # earth() loads "picture.png" from the working directory (main.cpp:93)
+    subprocess.run([exe, dump], check=True, cwd=os.path.dirname(O.EARTH_PNG))
     text = open(dump).read()
     parts = dict(re.findall(r"@@(\w+)\n(.*?)(?=@@|\Z)", text, flags=re.S))
     for n in BUILDERS:

@@ -46,7 +46,7 @@ _scenes = {}
 
 def _scene(name):
     if name not in _scenes:
-        _scenes[name] = rtnw.Scene.builtin(name)
+        _scenes[name] = rtnw.Scene.builtin(name, earth_png=O.EARTH_PNG)
     return _scenes[name]
 
 
@@ -64,6 +64,7 @@ CASES = [   # (scene, nx, ny, spp, chunk, seed)  — c1..c4 of BASELINE.json at 
     ("simple_light", 32, 16, 8, 8, 6),
     ("test", 32, 16, 8, 3, 7),
     ("two_spheres", 24, 24, 4, 4, 8),
+    ("earth", 32, 32, 8, 8, 9),
 ]
 
 
@@ -80,7 +81,8 @@ def test_gpu_matches_oracle(scene, nx, ny, ns, chunk, seed):
     assert exact > 0.5
 
 
-@pytest.mark.parametrize("name", ["c1_random", "c2_cornell", "c3_motion", "c4_final", "smoke", "simple_light"])
+@pytest.mark.parametrize("name", ["c1_random", "c2_cornell", "c3_motion", "c4_final", "smoke", "simple_light",
+                                  "earth"])
 def test_gpu_matches_reference_framebuffer(golden, name):
     """Against the reference's own counter-RNG output (golden, made by the reference binary)."""
     c = golden["counter_fb"][name]

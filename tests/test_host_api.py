@@ -36,7 +36,7 @@ def test_library_has_gfx950_code_object():
 
 @pytest.mark.parametrize("scene", list(O.SCENES))
 def test_scene_builders_match_reference(golden, scene):
-    d = rtnw.SceneDesc.builtin(scene)
+    d = rtnw.SceneDesc.builtin(scene, earth_png=O.EARTH_PNG)
     text = d.dump()
     assert hashlib.sha256(text.encode()).hexdigest() == golden["scene_dump_sha256"][scene]
     assert text == O.scene_dump(scene)
