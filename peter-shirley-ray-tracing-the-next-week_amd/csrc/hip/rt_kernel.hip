@@ -69,11 +69,10 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t seed, uint32_t pixel, ui
     return mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) ^ (((uint64_t)pixel << 32) | sample));
 }
 struct Rng {
-    uint64_t key;
+    uint64_t ctr;    // key + n*GAMMA for the last draw n (n = 0 after start)
     uint64_t mkey;   // medium stream key, derived once per sample
-    uint32_t n;
-    __device__ __forceinline__ void start(uint64_t k) { key = k; n = 0; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
-    __device__ __forceinline__ double next() { ++n; return u48(mix64(key + (uint64_t)n * kGamma)); }
+    __device__ __forceinline__ void start(uint64_t k) { ctr = k; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
+    __device__ __forceinline__ double next() { ctr += kGamma; return u48(mix64(ctr)); }
     __device__ __forceinline__ double medium(int bounce, int k) const {
         uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
         return u48(mix64(mkey + (m + 1) * kGamma));
@@ -301,95 +300,96 @@ __device__ __forceinline__ float boundary_t(const float4 *B, const float4 *insts
 }
 
 // ----------------------------------------------------------------- Perlin
-__device__ float perlin_noise(const float4 *ranvec, const int *perm, V3 p) {   // perlin.h:43-61, 25-39
+// One noise() (perlin.h:43-61, 25-39).  The six permutation reads are issued
+// together, then the eight gradient reads: two memory round trips per call.
+__device__ __forceinline__ float perlin_noise(const float4 *ranvec, const int *perm, V3 p) {
     float u = p.x - floorf(p.x);
     float v = p.y - floorf(p.y);
     float w = p.z - floorf(p.z);
     u = u * u * (3 - 2 * u);
     v = v * v * (3 - 2 * v);
     w = w * w * (3 - 2 * w);
-    int i = (int)floorf(p.x);
-    int j = (int)floorf(p.y);
-    int k = (int)floorf(p.z);
-    float uu = u * u * (3 - 2 * u);
-    float vv = v * v * (3 - 2 * v);
-    float ww = w * w * (3 - 2 * w);
+    const int i = (int)floorf(p.x);
+    const int j = (int)floorf(p.y);
+    const int k = (int)floorf(p.z);
+    const float uu = u * u * (3 - 2 * u);
+    const float vv = v * v * (3 - 2 * v);
+    const float ww = w * w * (3 - 2 * w);
+    const int px[2] = {perm[i & 255], perm[(i + 1) & 255]};
+    const int py[2] = {perm[256 + (j & 255)], perm[256 + ((j + 1) & 255)]};
+    const int pz[2] = {perm[512 + (k & 255)], perm[512 + ((k + 1) & 255)]};
     float accum = 0;   // corner order i, j, k as perlin_interp sums them
 #pragma unroll 1
-    for (int a = 0; a < 2; a++)
-#pragma unroll 1
-        for (int b = 0; b < 2; b++)
+    for (int a = 0; a < 2; ++a) {
+        V3 g[4];
 #pragma unroll
-            for (int d = 0; d < 2; d++) {
-                int h = perm[(i + a) & 255] ^ perm[256 + ((j + b) & 255)] ^ perm[512 + ((k + d) & 255)];
-                float4 g = ranvec[h];
-                V3 weight_v = mk(u - a, v - b, w - d);
-                accum += (a * uu + (1 - a) * (1 - uu)) * (b * vv + (1 - b) * (1 - vv)) *
-                         (d * ww + (1 - d) * (1 - ww)) * dot(mk(g.x, g.y, g.z), weight_v);
-            }
+        for (int c = 0; c < 4; ++c) {
+            const float4 t = ranvec[px[a] ^ py[c >> 1] ^ pz[c & 1]];
+            g[c] = mk(t.x, t.y, t.z);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int b = c >> 1, d = c & 1;
+            V3 weight_v = mk(u - a, v - b, w - d);
+            accum += (a * uu + (1 - a) * (1 - uu)) * (b * vv + (1 - b) * (1 - vv)) * (d * ww + (1 - d) * (1 - ww)) *
+                     dot(g[c], weight_v);
+        }
+    }
     return accum;
 }
 
-__device__ float perlin_turb(const float4 *ranvec, const int *perm, V3 p) {   // perlin.h:64-74
-    float accum = 0;
-    V3 temp_p = p;
-    float weight = 1.0f;
-#pragma unroll 1
-    for (int i = 0; i < 7; i++) {
-        accum += weight * perlin_noise(ranvec, perm, temp_p);
-        weight = (float)((double)weight * 0.5);
-        temp_p = mk(temp_p.x * 2, temp_p.y * 2, temp_p.z * 2);
+// Texture chain of one lane down to its leaf: checker_texture picks a child by
+// the sign of the sines (texture.h:35-44).  Returns the leaf kind (-1: chain too deep).
+__device__ __forceinline__ int tex_leaf(const RtKernelArgs &A, int ti, V3 p, float4 &t0, float4 &t1) {
+    for (int guard = 0; guard < RT_MAX_CHECKER_DEPTH; ++guard) {
+        t0 = A.texs[ti * 2 + 0];
+        t1 = A.texs[ti * 2 + 1];
+        const int kind = fbits(t0.x);
+        if (kind != RT_TEX_CHECKER) return kind;
+        float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+        ti = (sines < 0) ? fbits(t0.z) : fbits(t0.y);
     }
-    return fabsf(accum);
+    return -1;
 }
 
-template <bool kCount>
-__device__ V3 tex_value(const RtKernelArgs &A, int ti, float u, float v, V3 p, Counters &cnt) {   // texture.h:16-59
-    for (int guard = 0; guard < RT_MAX_CHECKER_DEPTH; ++guard) {
-        const float4 t0 = A.texs[ti * 2 + 0];
-        const float4 t1 = A.texs[ti * 2 + 1];
-        int kind = fbits(t0.x);
-        if (kind == RT_TEX_CONSTANT) return mk(t1.x, t1.y, t1.z);
-        if (kind == RT_TEX_CHECKER) {
-            float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
-            ti = (sines < 0) ? fbits(t0.z) : fbits(t0.y);
-            continue;
-        }
-        if (kind == RT_TEX_IMAGE) {   // surface_texture.h:19-30 (stride 3 as the reference addresses it)
-            const int nx = fbits(t0.y), ny = fbits(t0.z);
-            const uint8_t *data = A.texels + fbits(t0.w);
-            int i = (int)((1 - u) * nx);
-            int j = (int)((double)((1 - v) * ny) - 0.001);
-            if (i < 0) i = 0;
-            if (j < 0) j = 0;
-            if (i > nx - 1) i = nx - 1;
-            if (j > ny - 1) j = ny - 1;
-            const float r = (float)((int)data[3 * i + 3 * nx * j] / 255.0);
-            const float gg = (float)((int)data[3 * i + 3 * nx * j + 1] / 255.0);
-            const float b = (float)((int)data[3 * i + 3 * nx * j + 2] / 255.0);
-            return mk(r, gg, b);
-        }
-        // RT_TEX_NOISE
-        if (kCount) cnt.noise++;
-        float sc = t0.w;
-        float s = 1 + sinf(sc * p.x + 5 * perlin_turb(A.ranvec, A.perm, scale(sc, p)));
-        float h = 0.5f * 1;
-        return mk(s * h, s * h, s * h);
+// texture::value of a constant or image leaf (texture.h:16-27; surface_texture.h:19-30);
+// the noise leaf is finished after coop_turb.
+__device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, float4 t0, float4 t1, float u, float v) {
+    if (kind == RT_TEX_CONSTANT) return mk(t1.x, t1.y, t1.z);
+    if (kind == RT_TEX_IMAGE) {   // stride 3 as the reference addresses it
+        const int nx = fbits(t0.y), ny = fbits(t0.z);
+        const uint8_t *data = A.texels + fbits(t0.w);
+        int i = (int)((1 - u) * nx);
+        int j = (int)((double)((1 - v) * ny) - 0.001);
+        if (i < 0) i = 0;
+        if (j < 0) j = 0;
+        if (i > nx - 1) i = nx - 1;
+        if (j > ny - 1) j = ny - 1;
+        const float r = (float)((int)data[3 * i + 3 * nx * j] / 255.0);
+        const float gg = (float)((int)data[3 * i + 3 * nx * j + 1] / 255.0);
+        const float b = (float)((int)data[3 * i + 3 * nx * j + 2] / 255.0);
+        return mk(r, gg, b);
     }
     return mk(0, 0, 0);
 }
 
 // --------------------------------------------------------------- scatter
-template <bool kCount>
-__device__ __forceinline__ V3 random_in_unit_sphere(Rng &g, Counters &cnt) {   // material.h:41-47
-    V3 p;
-    do {
-        if (kCount) { cnt.l_rius++; if (first_active()) cnt.w_rius++; }
-        double x = g.next(), y = g.next(), z = g.next();
+// Candidates of the two rejection loops: `base` is the stream counter before the
+// candidate's first draw.
+struct SphereCand {   // material.h:41-47 random_in_unit_sphere
+    __device__ __forceinline__ bool operator()(uint64_t base, V3 &p) const {
+        const double x = u48(mix64(base + kGamma)), y = u48(mix64(base + 2 * kGamma)), z = u48(mix64(base + 3 * kGamma));
         p = sub(scale(2.0f, mk((float)x, (float)y, (float)z)), mk(1, 1, 1));
-    } while ((double)dot(p, p) >= 1.0);
-    return p;
-}
+        return (double)dot(p, p) < 1.0;
+    }
+};
+struct DiskCand {     // camera.h:6-12 random_in_unit_disk
+    __device__ __forceinline__ bool operator()(uint64_t base, V3 &p) const {
+        const double a = u48(mix64(base + kGamma)), b = u48(mix64(base + 2 * kGamma));
+        p = sub(scale(2.0f, mk((float)a, (float)b, 0)), mk(1, 1, 0));
+        return (double)dot(p, p) < 1.0;
+    }
+};
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(2 * dot(v, n), n)); }   // material.h:36-38
 
 // ------------------------------------------------------------ work claim
@@ -399,6 +399,120 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 }
 
 constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
+
+// ------------------------------------------- cooperative rejection sampling
+// The rejection loops of the reference (camera.h:6-12 random_in_unit_disk,
+// material.h:41-47 random_in_unit_sphere) accept the first candidate inside the
+// unit ball; candidate c of a loop entered after draw n uses draws n+K*c+1 ..
+// n+K*c+K.  Counter streams are random access, so the wave evaluates the
+// candidates of all lanes that need a point at once: the m requesting lanes
+// publish (stream position) in LDS slots 0..m-1 and all 64 lanes take candidates
+// round-robin (lane L evaluates candidate c0 + L/m of slot L%m).  Each owner keeps
+// its lowest accepted candidate, so the point and the draws consumed are exactly
+// those of its own sequential loop; rounds repeat for owners whose candidates all
+// failed.  A lane loop that ran ~6 wave trips at ~16% SIMD efficiency (the
+// slowest lane of 48 decides) takes ~2-3 fully used trips.
+// Must be called with all 64 lanes of the wave active.
+struct CoopSlot {
+    uint64_t ctr;
+    uint64_t pad;
+};
+
+template <int K, bool kCount, class Cand>
+__device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt, Cand cand) {
+    V3 res = mk(0, 0, 0);
+    bool pending = want;
+    uint64_t U = __ballot(pending);
+    while (U != 0ull) {
+        const uint32_t m = (uint32_t)__popcll(U);            // wave-uniform
+        uint64_t P = 0;                                        // lanes congruent to 0 mod m
+        for (uint32_t b = 0; b < 64; b += m) P |= 1ull << b;
+        const uint32_t r = lanes_below(U);
+        if (pending) slots[r].ctr = g.ctr;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // t = lane / m exactly: lane < 64, m <= 64, inv = ceil(2^16 / m)
+        const uint32_t inv = (0xFFFFu + m) / m;
+        const uint32_t t = (lane * inv) >> 16;
+        const uint32_t slot = lane - t * m;
+        const uint64_t base = slots[slot].ctr + (uint64_t)(K * t) * kGamma;
+        V3 p;
+        const bool ok = cand(base, p);
+        const uint64_t okm = __ballot(ok);
+        if (kCount && first_active()) cnt.w_rius++;
+        uint32_t src = lane;
+        bool won = false;
+        if (pending) {
+            const uint64_t mine = P << r;
+            const uint64_t win = okm & mine;
+            if (win != 0ull) {
+                src = (uint32_t)__builtin_ctzll(win);
+                const uint32_t tried = (uint32_t)__popcll(mine & ((1ull << src) - 1ull)) + 1u;
+                g.ctr += (uint64_t)(K * tried) * kGamma;
+                if (kCount) cnt.l_rius += tried;
+                won = true;
+                pending = false;
+            } else {
+                const uint32_t tried = (uint32_t)__popcll(mine);
+                g.ctr += (uint64_t)(K * tried) * kGamma;
+                if (kCount) cnt.l_rius += tried;
+            }
+        }
+        // every lane takes part in the exchange (bpermute reads the source lane's register)
+        const float px = __shfl(p.x, (int)src), py = __shfl(p.y, (int)src), pz = __shfl(p.z, (int)src);
+        if (won) res = mk(px, py, pz);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        U = __ballot(pending);
+    }
+    return res;
+}
+
+// Cooperative turbulence (perlin.h:64-74).  Octave k of turb(q) is
+// noise(q * 2^k) weighted 2^-k: `temp_p *= 2` and `weight *= 0.5` are exact, so
+// the octaves are independent.  The lanes that need turb publish q in LDS and the
+// wave evaluates the 7 octaves of up to 9 of them at once, one noise() per lane;
+// each owner gathers its 7 values and sums them in octave order, exactly as the
+// reference's loop does.  A wave with one noisy lane used to run all 7 octaves as
+// a chain of 28 dependent gathers; now it runs one noise() per round.
+// Must be called with all 64 lanes of the wave active.
+__device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec, const int *perm, CoopSlot *slots,
+                                           uint32_t lane) {
+    const uint64_t U = __ballot(want);
+    if (U == 0ull) return 0.f;
+    float res = 0.f;
+    const uint32_t m = (uint32_t)__popcll(U);
+    const uint32_t r = lanes_below(U);
+    float4 *pts = reinterpret_cast<float4 *>(slots);
+    if (want) pts[r] = make_float4(q.x, q.y, q.z, 0.f);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t lo = lane / 7, oct = lane - lo * 7;
+    for (uint32_t base = 0; base < m; base += 9) {
+        const uint32_t o = base + lo;
+        float val = 0.f;
+        if (lane < 63 && o < m) {
+            const float4 pt = pts[o];
+            const float s = (float)(1u << oct);
+            val = perlin_noise(ranvec, perm, mk(pt.x * s, pt.y * s, pt.z * s));
+        }
+        const bool mine = want && r >= base && r < base + 9;
+        const uint32_t src0 = ((r - base) * 7u) & 63u;
+        float acc = 0.f, weight = 1.0f;
+#pragma unroll
+        for (int kk = 0; kk < 7; ++kk) {
+            const float nk = __shfl(val, (int)((src0 + kk) & 63u));
+            acc += weight * nk;
+            weight = (float)((double)weight * 0.5);
+        }
+        if (mine) res = fabsf(acc);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    return res;
+}
 
 // Minimum waves per SIMD the register allocation must allow (launch_bounds second
 // argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  Traversal is latency-bound, so
@@ -421,8 +535,10 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 template <bool kCount, bool kProf>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
+    __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
     const uint32_t lane = lane_id();
     uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
+    CoopSlot *slots = lds_slots[threadIdx.x >> 6];
 
     // wave-uniform claim pool
     uint32_t pool_next = 0, pool_end = 0;
@@ -438,7 +554,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
     r.o = mk(0, 0, 0); r.d = mk(0, 0, 0); r.time = 0;
     V3 beta = mk(1, 1, 1);
     int depth = 0;
-    Rng g; g.key = 0; g.mkey = 0; g.n = 0;
+    Rng g; g.ctr = 0; g.mkey = 0;
     uint32_t px = 0, py = 0;
     uint32_t node = 0;
     int sp = 0;
@@ -506,23 +622,23 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         if (__ballot(!finished) == 0ull) break;
 
         // ---- 2. start camera samples (main.cpp:305-308, camera.h:41-56) ------
-        if (phase == PH_IDLE && !finished) {
+        const bool starting = phase == PH_IDLE && !finished;
+        float cu_ = 0, cv_ = 0;
+        if (starting) {
             int j = A.ny - 1 - (int)py;
             g.start(sample_key(A.seed, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
-            float u = (float)((double)(int)px + g.next()) / (float)A.nx;
-            float v = (float)((double)j + g.next()) / (float)A.ny;
-            V3 p;
-            do {
-                double a = g.next(), b = g.next();
-                p = sub(scale(2.0f, mk((float)a, (float)b, 0)), mk(1, 1, 0));
-            } while ((double)dot(p, p) >= 1.0);
-            V3 rd = scale(A.lens, p);
+            cu_ = (float)((double)(int)px + g.next()) / (float)A.nx;
+            cv_ = (float)((double)j + g.next()) / (float)A.ny;
+        }
+        const V3 disk = coop_reject<2, kCount>(starting, g, slots, lane, cnt, DiskCand());
+        if (starting) {
+            V3 rd = scale(A.lens, disk);
             V3 cu = mk(A.cu[0], A.cu[1], A.cu[2]), cv = mk(A.cv[0], A.cv[1], A.cv[2]);
             V3 offset = add(scale(rd.x, cu), scale(rd.y, cv));
             float time = (float)((double)A.ct0 + g.next() * (double)(A.ct1 - A.ct0));
             V3 org = mk(A.org[0], A.org[1], A.org[2]);
-            V3 dir = sub(sub(add(add(mk(A.llc[0], A.llc[1], A.llc[2]), scale(u, mk(A.hor[0], A.hor[1], A.hor[2]))),
-                                 scale(v, mk(A.ver[0], A.ver[1], A.ver[2]))), org), offset);
+            V3 dir = sub(sub(add(add(mk(A.llc[0], A.llc[1], A.llc[2]), scale(cu_, mk(A.hor[0], A.hor[1], A.hor[2]))),
+                                 scale(cv_, mk(A.ver[0], A.ver[1], A.ver[2]))), org), offset);
             r.o = add(org, offset);
             r.d = dir;
             r.time = time;
@@ -597,168 +713,193 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             }
         }
         mark(1);
-        if (phase != PH_READY) continue;   // still searching: carry on next iteration
+        // Lanes still searching carry on in the next iteration; the others shade.
+        // Stages 4-5 keep the whole wave active (the cooperative sampler needs it).
+        const bool ready = phase == PH_READY;
 
         // ---- 4. media after the surfaces (constant_medium.h:26-50) -------------
-        bool have = best_prim != 0xFFFFFFFFu;
+        bool have = false;
         Hit hr;
-        if (have) hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
-        for (int k = 0; k < A.nmedia; ++k) {
-            if (kCount) cnt.media++;
-            const int4 md = A.media[k];
-            float r1, r2;
-            const float4 bm = A.bprims[md.x * 4 + 3];
-            if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {
-                // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
-                if (kCount) cnt.spheres++;
-                const float4 sg = A.bprims[md.x * 4 + 0];
-                V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
-                float a = dot(r.d, r.d);
-                float b = dot(oc, r.d);
-                float cc = dot(oc, oc) - sg.w * sg.w;
-                float disc = b * b - a * cc;
-                if (!(disc > 0)) continue;
-                const float ta = (-b - sqrtf(disc)) / a;
-                const float tb = (-b + sqrtf(disc)) / a;
-                if (ta < RT_FLT_MAX && ta > -RT_FLT_MAX) r1 = ta;
-                else if (tb < RT_FLT_MAX && tb > -RT_FLT_MAX) r1 = tb;
-                else continue;
-                const float tmin2 = (float)((double)r1 + 0.0001);
-                if (ta < RT_FLT_MAX && ta > tmin2) r2 = ta;
-                else if (tb < RT_FLT_MAX && tb > tmin2) r2 = tb;
-                else continue;
-            } else {
-                r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
-                if (r1 == RT_INF) continue;
-                r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
-                if (r2 == RT_INF) continue;
-            }
-            float tmax = have ? best_t : RT_FLT_MAX;
-            if (r1 < A.tmin) r1 = A.tmin;
-            if (r2 > tmax) r2 = tmax;
-            if (r1 >= r2) continue;
-            if (r1 < 0) r1 = 0;
-            float dlen = len(r.d);
-            float distance_inside_boundary = (r2 - r1) * dlen;
-            float density = __int_as_float(md.z);
-            float hit_distance = (float)((double)(-(1 / density)) * log(g.medium(depth, k)));
-            if (hit_distance < distance_inside_boundary) {
-                best_t = r1 + hit_distance / dlen;
-                have = true;
-                hr.p = at(r, best_t);
-                hr.n = mk(1, 0, 0);
-                hr.u = 0.f;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
-                hr.v = 0.f;
-                hr.mat = md.w;
+        hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
+        if (ready) {
+            have = best_prim != 0xFFFFFFFFu;
+            if (have) hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
+            for (int k = 0; k < A.nmedia; ++k) {
+                if (kCount) cnt.media++;
+                const int4 md = A.media[k];
+                float r1, r2;
+                const float4 bm = A.bprims[md.x * 4 + 3];
+                if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {
+                    // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
+                    if (kCount) cnt.spheres++;
+                    const float4 sg = A.bprims[md.x * 4 + 0];
+                    V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
+                    float a = dot(r.d, r.d);
+                    float b = dot(oc, r.d);
+                    float cc = dot(oc, oc) - sg.w * sg.w;
+                    float disc = b * b - a * cc;
+                    if (!(disc > 0)) continue;
+                    const float ta = (-b - sqrtf(disc)) / a;
+                    const float tb = (-b + sqrtf(disc)) / a;
+                    if (ta < RT_FLT_MAX && ta > -RT_FLT_MAX) r1 = ta;
+                    else if (tb < RT_FLT_MAX && tb > -RT_FLT_MAX) r1 = tb;
+                    else continue;
+                    const float tmin2 = (float)((double)r1 + 0.0001);
+                    if (ta < RT_FLT_MAX && ta > tmin2) r2 = ta;
+                    else if (tb < RT_FLT_MAX && tb > tmin2) r2 = tb;
+                    else continue;
+                } else {
+                    r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
+                    if (r1 == RT_INF) continue;
+                    r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
+                    if (r2 == RT_INF) continue;
+                }
+                float tmax = have ? best_t : RT_FLT_MAX;
+                if (r1 < A.tmin) r1 = A.tmin;
+                if (r2 > tmax) r2 = tmax;
+                if (r1 >= r2) continue;
+                if (r1 < 0) r1 = 0;
+                float dlen = len(r.d);
+                float distance_inside_boundary = (r2 - r1) * dlen;
+                float density = __int_as_float(md.z);
+                float hit_distance = (float)((double)(-(1 / density)) * log(g.medium(depth, k)));
+                if (hit_distance < distance_inside_boundary) {
+                    best_t = r1 + hit_distance / dlen;
+                    have = true;
+                    hr.p = at(r, best_t);
+                    hr.n = mk(1, 0, 0);
+                    hr.u = 0.f;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
+                    hr.v = 0.f;
+                    hr.mat = md.w;
+                }
             }
         }
 
         mark(2);
         // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
-        V3 L;
-        bool terminate = true;
-        if (!have) {
-            if (A.background == RT_BG_SKY) {                                  // TNW/Chapter03:29-31
-                V3 ud = unit(r.d);
-                float t = (float)(0.5 * ((double)ud.y + 1.0));
-                V3 sky = add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
-                L = mul(beta, sky);
-            } else {
-                L = mul(beta, mk(0, 0, 0));
-            }
-        } else {
+        // The per-material work that dominates (texture lookup, the rejection loop
+        // of random_in_unit_sphere) runs ONCE for every lane that needs it instead
+        // of once per material branch; each lane still makes exactly the draws its
+        // own material makes, in the same order (one material per lane).
+        const bool shading = ready && have;
+        int kind = -1;
+        bool live = false, noisy = false;
+        float nscale = 0.f;
+        V3 tv = mk(0, 0, 0);
+        if (shading) {
             if (kCount) cnt.shades++;
-            const float4 m0 = A.mats[hr.mat * 2 + 0];
-            const float4 m1 = A.mats[hr.mat * 2 + 1];
-            const int kind = fbits(m0.x);
-            const int tex = fbits(m0.y);
-            // The per-material work that dominates (texture lookup, the rejection loop
-            // of random_in_unit_sphere) runs ONCE for every lane that needs it instead
-            // of once per material branch; each lane still makes exactly the draws its
-            // own material makes, in the same order (one material per lane).
-            const bool live = depth < A.max_depth;
+            kind = fbits(A.mats[hr.mat * 2 + 0].x);
+            live = depth < A.max_depth;
             const bool textured = kind == RT_MAT_DIFFUSE_LIGHT ||
                                   (live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC));
-            V3 tv = mk(0, 0, 0);
-            if (textured) tv = tex_value<kCount>(A, tex, hr.u, hr.v, hr.p, cnt);          // texture.h / perlin.h
-            const bool wants_sphere = live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_METAL ||
-                                               kind == RT_MAT_ISOTROPIC);
-            V3 rius = mk(0, 0, 0);
-            if (wants_sphere) rius = random_in_unit_sphere<kCount>(g, cnt);   // material.h:41-47
-            V3 emitted = kind == RT_MAT_DIFFUSE_LIGHT ? tv : mk(0, 0, 0);
-            bool scattered = false;
-            V3 att = mk(0, 0, 0);
-            Ray ns;
-            if (live) {
-                if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
-                    V3 target = add(add(hr.p, hr.n), rius);
-                    ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
-                    att = tv;
-                    scattered = true;
-                } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
-                    V3 reflected = reflect(unit(r.d), hr.n);
-                    ns.o = hr.p; ns.d = add(reflected, scale(m0.z, rius)); ns.time = 0.0f;
-                    att = mk(m1.x, m1.y, m1.z);
-                    scattered = dot(ns.d, hr.n) > 0;
-                } else if (kind == RT_MAT_DIELECTRIC) {                       // material.h:90-120
-                    const float ref_idx = m0.w;
-                    V3 outward_normal;
-                    V3 reflected = reflect(r.d, hr.n);
-                    float ni_over_nt, cosine;
-                    att = mk(1.0f, 1.0f, 1.0f);
-                    float dn = dot(r.d, hr.n);
-                    if (dn > 0) {
-                        outward_normal = neg(hr.n);
-                        ni_over_nt = ref_idx;
-                        cosine = dot(r.d, hr.n) / len(r.d);
-                        cosine = sqrtf(1 - ref_idx * ref_idx * (1 - cosine * cosine));
-                    } else {
-                        outward_normal = hr.n;
-                        ni_over_nt = (float)(1.0 / (double)ref_idx);
-                        cosine = -dot(r.d, hr.n) / len(r.d);
-                    }
-                    // refract, material.h:23-33
-                    V3 uv = unit(r.d);
-                    float dt = dot(uv, outward_normal);
-                    float disc = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
-                    float reflect_prob;
-                    V3 refracted = mk(0, 0, 0);
-                    if (disc > 0) {
-                        refracted = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))),
-                                        scale(sqrtf(disc), outward_normal));
-                        // schlick, material.h:16-20
-                        float r0 = (1 - ref_idx) / (1 + ref_idx);
-                        r0 = r0 * r0;
-                        reflect_prob = (float)(r0 + (double)(1 - r0) * pow5((double)(1 - cosine)));
-                    } else {
-                        reflect_prob = 1.0f;
-                    }
-                    ns.o = hr.p; ns.time = 0.0f;
-                    ns.d = (g.next() < (double)reflect_prob) ? reflected : refracted;
-                    scattered = true;
-                } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
-                    ns.o = hr.p; ns.d = rius; ns.time = 0.0f;
-                    att = tv;
-                    scattered = true;
-                }
-            }
-            if (scattered) {
-                beta = mul(beta, att);
-                r = ns;
-                ++depth;
-                terminate = false;
-                begin_segment();
-            } else {
-                L = mul(beta, emitted);
+            if (textured) {
+                float4 t0, t1;
+                const int tkind = tex_leaf(A, fbits(A.mats[hr.mat * 2 + 0].y), hr.p, t0, t1);   // texture.h:35-44
+                noisy = tkind == RT_TEX_NOISE;
+                nscale = t0.w;
+                if (!noisy) tv = tex_value_leaf(A, tkind, t0, t1, hr.u, hr.v);
             }
         }
-        if (terminate) {
-            if (!(L.x == L.x)) L.x = 0;                                       // de_nan, main.cpp:232-242
-            if (!(L.y == L.y)) L.y = 0;
-            if (!(L.z == L.z)) L.z = 0;
-            part = add(part, L);
-            ++s_cur;
-            phase = PH_IDLE;
+        if (kCount && noisy) cnt.noise++;
+        const float turb = coop_turb(noisy, scale(nscale, hr.p), A.ranvec, A.perm, slots, lane);   // perlin.h:64-74
+        if (noisy) {                                                                               // texture.h:52-56
+            const float sv = 1 + sinf(nscale * hr.p.x + 5 * turb);
+            const float h = 0.5f * 1;
+            tv = mk(sv * h, sv * h, sv * h);
+        }
+        const bool wants_sphere = shading && live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_METAL ||
+                                                      kind == RT_MAT_ISOTROPIC);
+        const V3 rius = coop_reject<3, kCount>(wants_sphere, g, slots, lane, cnt, SphereCand());   // material.h:41-47
+        if (ready) {
+            V3 L;
+            bool terminate = true;
+            if (!have) {
+                if (A.background == RT_BG_SKY) {                                  // TNW/Chapter03:29-31
+                    V3 ud = unit(r.d);
+                    float t = (float)(0.5 * ((double)ud.y + 1.0));
+                    V3 sky = add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
+                    L = mul(beta, sky);
+                } else {
+                    L = mul(beta, mk(0, 0, 0));
+                }
+            } else {
+                const float4 m0 = A.mats[hr.mat * 2 + 0];
+                const float4 m1 = A.mats[hr.mat * 2 + 1];
+                V3 emitted = kind == RT_MAT_DIFFUSE_LIGHT ? tv : mk(0, 0, 0);
+                bool scattered = false;
+                V3 att = mk(0, 0, 0);
+                Ray ns;
+                if (live) {
+                    if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
+                        V3 target = add(add(hr.p, hr.n), rius);
+                        ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
+                        att = tv;
+                        scattered = true;
+                    } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
+                        V3 reflected = reflect(unit(r.d), hr.n);
+                        ns.o = hr.p; ns.d = add(reflected, scale(m0.z, rius)); ns.time = 0.0f;
+                        att = mk(m1.x, m1.y, m1.z);
+                        scattered = dot(ns.d, hr.n) > 0;
+                    } else if (kind == RT_MAT_DIELECTRIC) {                       // material.h:90-120
+                        const float ref_idx = m0.w;
+                        V3 outward_normal;
+                        V3 reflected = reflect(r.d, hr.n);
+                        float ni_over_nt, cosine;
+                        att = mk(1.0f, 1.0f, 1.0f);
+                        float dn = dot(r.d, hr.n);
+                        if (dn > 0) {
+                            outward_normal = neg(hr.n);
+                            ni_over_nt = ref_idx;
+                            cosine = dot(r.d, hr.n) / len(r.d);
+                            cosine = sqrtf(1 - ref_idx * ref_idx * (1 - cosine * cosine));
+                        } else {
+                            outward_normal = hr.n;
+                            ni_over_nt = (float)(1.0 / (double)ref_idx);
+                            cosine = -dot(r.d, hr.n) / len(r.d);
+                        }
+                        // refract, material.h:23-33
+                        V3 uv = unit(r.d);
+                        float dt = dot(uv, outward_normal);
+                        float disc = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
+                        float reflect_prob;
+                        V3 refracted = mk(0, 0, 0);
+                        if (disc > 0) {
+                            refracted = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))),
+                                            scale(sqrtf(disc), outward_normal));
+                            // schlick, material.h:16-20
+                            float r0 = (1 - ref_idx) / (1 + ref_idx);
+                            r0 = r0 * r0;
+                            reflect_prob = (float)(r0 + (double)(1 - r0) * pow5((double)(1 - cosine)));
+                        } else {
+                            reflect_prob = 1.0f;
+                        }
+                        ns.o = hr.p; ns.time = 0.0f;
+                        ns.d = (g.next() < (double)reflect_prob) ? reflected : refracted;
+                        scattered = true;
+                    } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
+                        ns.o = hr.p; ns.d = rius; ns.time = 0.0f;
+                        att = tv;
+                        scattered = true;
+                    }
+                }
+                if (scattered) {
+                    beta = mul(beta, att);
+                    r = ns;
+                    ++depth;
+                    terminate = false;
+                    begin_segment();
+                } else {
+                    L = mul(beta, emitted);
+                }
+            }
+            if (terminate) {
+                if (!(L.x == L.x)) L.x = 0;                                       // de_nan, main.cpp:232-242
+                if (!(L.y == L.y)) L.y = 0;
+                if (!(L.z == L.z)) L.z = 0;
+                part = add(part, L);
+                ++s_cur;
+                phase = PH_IDLE;
+            }
         }
         mark(3);
     }

@@ -36,19 +36,16 @@ for step in "$@"; do
             run pmc_l2 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     pmc_sq) export TMPDIR=/tmp
             run pmc_sq 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
-    ab)     run ab 1200 python3 tools/ab.py peter-shirley-ray-tracing-the-next-week_amd/librt_hip.so variants/w3/librt_hip.so variants/w4/librt_hip.so --rounds 2 ;;
     stages) run stages 600 python3 tools/stage_profile.py final ;;
     stages_cornell) run stages_cornell 600 python3 tools/stage_profile.py cornell_box ;;
     dist2)  run dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --dist-backend gloo --spp 64 --steps 2 --warmup 1 --ppm gpurun_out/dist2.ppm ;;
     one_ppm) run one_ppm 600 python3 bench.py --spp 64 --steps 1 --warmup 0 --no-cpu-baseline --ppm gpurun_out/one.ppm ;;
-    ab5)    run ab5 1200 python3 tools/ab.py peter-shirley-ray-tracing-the-next-week_amd/librt_hip.so variants/w3/librt_hip.so variants/w5/librt_hip.so --rounds 2 ;;
     pmc)    export TMPDIR=/tmp
             run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
             run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
             run pmc_l2 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
             run pmc_sq 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
-    ab_trav) run ab_trav 1200 python3 tools/ab.py variants/ww/librt_hip.so variants/ifif/librt_hip.so variants/ww/librt_hip.so:RTNW_BVH_MAX_LEAF=4 variants/ifif/librt_hip.so:RTNW_BVH_MAX_LEAF=4 variants/ww/librt_hip.so:RTNW_BVH_MAX_LEAF=2 --rounds 2 ;;
-    ab_batch) run ab_batch 1500 python3 tools/ab.py variants/b32/librt_hip.so variants/b40/librt_hip.so variants/b48/librt_hip.so variants/b56/librt_hip.so variants/b64/librt_hip.so --rounds 2 ;;
+    ab)     run ab 1200 python3 tools/ab.py $AB_LIBS --rounds ${AB_ROUNDS:-2} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
