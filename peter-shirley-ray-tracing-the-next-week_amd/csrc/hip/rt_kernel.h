@@ -8,7 +8,7 @@
 
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)
-    const float4 *nodes;    // 4 x float4 per BVH node
+    const float4 *nodes;    // BVH nodes, breadth-first: 4 x float4 (width 2) or 8 x float4 (width 4)
     const float4 *prims;    // 4 x float4 per surface primitive (leaf order)
     const float4 *bprims;   // 4 x float4 per media-boundary primitive
     const int4 *media;      // 1 x int4 per medium
@@ -19,6 +19,8 @@ struct RtKernelArgs {
     const int *perm;        // 3 x 256 Perlin permutations
     const uint8_t *texels;  // image_texture bytes
     uint32_t root;
+    uint32_t nnodes;
+    int bvh_width;          // 2 or 4
     int has_bvh;
     int nmedia;
     // camera (camera.h members)
@@ -43,4 +45,5 @@ struct RtKernelArgs {
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
-extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode);  // mode: 0 plain, 1 count, 2 profile
+// mode: 0 plain, 1 count, 2 profile; width: BVH width of the scene (2 or 4)
+extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);

@@ -97,6 +97,34 @@ __device__ __forceinline__ double pow5(double x) {
 __device__ __forceinline__ float4 ld4(const float4 *p, uint32_t i) { return p[i]; }
 __device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
 
+// BVH slab test primitives.  Packed FP32 FMA for the lo/hi plane pairs; min/max
+// as plain VALU ops: their operands are never signalling NaNs (FMA results, t_min,
+// the current best t), so the IEEE-mode quieting the compiler would add per use
+// of a loop-carried value is dead weight.  (minnum semantics: a NaN plane distance
+// from an axis-parallel ray leaves that axis unconstrained, i.e. conservative.)
+typedef float F2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ F2 pk_fma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float vmin(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // Ray into the object space of an instance chain (hitable.h:66-67, 129-135).
 __device__ __forceinline__ Ray to_object(const float4 *insts, int inst, Ray r) {
     const float4 *I = insts + inst * 7;
@@ -185,12 +213,9 @@ __device__ __forceinline__ float rect_t(int kind, float4 g0, float k, const Ray 
 // prim kinds: 0 sphere, 1 moving sphere, 2 xy, 3 xz, 4 yz  (rect axis = 2, 1, 0)
 __device__ __forceinline__ int rect_axis(int kind) { return 4 - kind; }
 
-__device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float tmin,
-                                        int &key, int &kind_out) {
-    const float4 g0 = P[idx * 4 + 0];
-    const float4 g1 = P[idx * 4 + 1];
-    const float4 g2 = P[idx * 4 + 2];
-    const float4 mm = P[idx * 4 + 3];
+// Test of one primitive whose 32-B head (g0, mm) is already loaded.
+__device__ __forceinline__ float prim_t_head(float4 g0, float4 mm, const float4 *P, const float4 *insts, uint32_t idx,
+                                             const Ray &r0, float tmin, int &key, int &kind_out) {
     int kind = fbits(mm.x) & 0xff;
     int inst = fbits(mm.z);
     int order = fbits(mm.w);
@@ -202,13 +227,18 @@ __device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, ui
         t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, r, tmin);
         key = order;
     } else if (kind == RT_PRIM_MOVING_SPHERE) {
-        t = sphere_t(msphere_center(g0, g1, g2, r.time), g0.w, r, tmin);
+        t = sphere_t(msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time), g0.w, r, tmin);
         key = order;
     } else {
-        t = rect_t(kind, g0, g1.x, r, tmin);
+        t = rect_t(kind, g0, mm.y, r, tmin);
         key = -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
     }
     return t;
+}
+
+__device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float tmin,
+                                        int &key, int &kind_out) {
+    return prim_t_head(P[idx * 4 + 0], P[idx * 4 + 1], P, insts, idx, r0, tmin, key, kind_out);
 }
 
 struct Hit { V3 p, n; float u, v; int mat; };
@@ -228,9 +258,7 @@ __device__ __forceinline__ void sphere_uv(V3 p, float &u, float &v) {
 __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts, const float4 *mats, uint32_t idx,
                                            const Ray &r0, float t) {
     const float4 g0 = P[idx * 4 + 0];
-    const float4 g1 = P[idx * 4 + 1];
-    const float4 g2 = P[idx * 4 + 2];
-    const float4 mm = P[idx * 4 + 3];
+    const float4 mm = P[idx * 4 + 1];
     int kind = fbits(mm.x) & 0xff;
     int flip = (fbits(mm.x) >> 8) & 1;
     int inst = fbits(mm.z);
@@ -241,14 +269,14 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
     if (kind == RT_PRIM_SPHERE) {
         h.n = divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w);
     } else if (kind == RT_PRIM_MOVING_SPHERE) {
-        h.n = divs(sub(h.p, msphere_center(g0, g1, g2, r.time)), g0.w);
+        h.n = divs(sub(h.p, msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time)), g0.w);
     } else {
         int axis = rect_axis(kind);
         h.n = mk(axis == 0 ? 1.f : 0.f, axis == 1 ? 1.f : 0.f, axis == 2 ? 1.f : 0.f);
     }
     h.u = 0.f;
     h.v = 0.f;
-    h.mat = fbits(mm.y);
+    h.mat = fbits(mm.x) >> 9;
     if (fbits(mats[h.mat * 2 + 1].w) & 1) {
         if (kind == RT_PRIM_SPHERE) {
             sphere_uv(divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w), h.u, h.v);   // sphere.h:36
@@ -371,6 +399,73 @@ __device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, fl
         return mk(r, gg, b);
     }
     return mk(0, 0, 0);
+}
+
+// ------------------------------------------------------------ BVH node step
+// Per-ray slab-test constants: 1/d (padded boxes need no exact division) and
+// -o/d, duplicated into packed pairs for v_pk_fma_f32.
+struct Slab { F2 ix, iy, iz, nox, noy, noz; float tmin; };
+__device__ __forceinline__ Slab make_slab(const Ray &r, float tmin) {
+    const float ix = __builtin_amdgcn_rcpf(r.d.x), iy = __builtin_amdgcn_rcpf(r.d.y), iz = __builtin_amdgcn_rcpf(r.d.z);
+    Slab s;
+    s.ix = F2{ix, ix}; s.iy = F2{iy, iy}; s.iz = F2{iz, iz};
+    s.nox = F2{-r.o.x * ix, -r.o.x * ix}; s.noy = F2{-r.o.y * iy, -r.o.y * iy}; s.noz = F2{-r.o.z * iz, -r.o.z * iz};
+    s.tmin = tmin;
+    return s;
+}
+// entry distance of one child box, +inf if the ray misses it (or the slot is empty)
+__device__ __forceinline__ float box_entry(const Slab &s, F2 x, F2 y, F2 z, float best_t, uint32_t c) {
+    const F2 a = pk_fma(x, s.ix, s.nox), b = pk_fma(y, s.iy, s.noy), e = pk_fma(z, s.iz, s.noz);
+    const float tn = vmax3(vmin(a.x, a.y), vmin(b.x, b.y), vmax(vmin(e.x, e.y), s.tmin));
+    const float tf = vmin3(vmax(a.x, a.y), vmax(b.x, b.y), vmin(vmax(e.x, e.y), best_t));
+    return (tn <= tf && c != RT_EMPTY_CHILD) ? tn : RT_INF;
+}
+__device__ __forceinline__ void cas(float &ka, uint32_t &ca, float &kb, uint32_t &cb) {
+    const bool sw = kb < ka;
+    const float tk = sw ? kb : ka;
+    kb = sw ? ka : kb;
+    ka = tk;
+    const uint32_t tc = sw ? cb : ca;
+    cb = sw ? ca : cb;
+    ca = tc;
+}
+// One interior node: test the children, push the hit ones but the nearest far to
+// near (branch-free: a slot is written, then kept only if the child was hit; the
+// builder bounds sp by RT_STACK_DEPTH - 1), return the nearest (or empty).
+template <int kWidth>
+__device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, float best_t, uint32_t *stk, int &sp) {
+    if (kWidth == 2) {   // rt_dnode2
+        const float4 b0 = N[0], b1 = N[1], b2 = N[2], cf = N[3];
+        const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
+        const float k0 = box_entry(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, c0);
+        const float k1 = box_entry(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, c1);
+        const bool second = k1 < k0;   // ties: child 0 first
+        const uint32_t nearc = second ? c1 : c0, farc = second ? c0 : c1;
+        const float kn = second ? k1 : k0, kf = second ? k0 : k1;
+        stk[sp * 64] = farc;
+        sp += kf != RT_INF;
+        return kn != RT_INF ? nearc : RT_EMPTY_CHILD;
+    } else {             // rt_dnode4
+        const float4 qx01 = N[0], qx23 = N[1], qy01 = N[2], qy23 = N[3], qz01 = N[4], qz23 = N[5], cf = N[6];
+        uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y), c2 = (uint32_t)fbits(cf.z),
+                 c3 = (uint32_t)fbits(cf.w);
+        float k0 = box_entry(s, F2{qx01.x, qx01.y}, F2{qy01.x, qy01.y}, F2{qz01.x, qz01.y}, best_t, c0);
+        float k1 = box_entry(s, F2{qx01.z, qx01.w}, F2{qy01.z, qy01.w}, F2{qz01.z, qz01.w}, best_t, c1);
+        float k2 = box_entry(s, F2{qx23.x, qx23.y}, F2{qy23.x, qy23.y}, F2{qz23.x, qz23.y}, best_t, c2);
+        float k3 = box_entry(s, F2{qx23.z, qx23.w}, F2{qy23.z, qy23.w}, F2{qz23.z, qz23.w}, best_t, c3);
+        cas(k0, c0, k1, c1);   // sorting network, nearest first
+        cas(k2, c2, k3, c3);
+        cas(k0, c0, k2, c2);
+        cas(k1, c1, k3, c3);
+        cas(k1, c1, k2, c2);
+        stk[sp * 64] = c3;
+        sp += k3 != RT_INF;
+        stk[sp * 64] = c2;
+        sp += k2 != RT_INF;
+        stk[sp * 64] = c1;
+        sp += k1 != RT_INF;
+        return k0 != RT_INF ? c0 : RT_EMPTY_CHILD;
+    }
 }
 
 // --------------------------------------------------------------- scatter
@@ -523,6 +618,12 @@ __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec
 #define RT_READY_BATCH 48
 #endif
 
+// float4 of BVH nodes kept in LDS per workgroup: 252 x 16 B fills the LDS left by
+// 4 workgroups per CU (stacks 32 KB + sampler slots 4 KB each): 63 BVH2 or 36 BVH4 nodes.
+#ifndef RT_LDS_NODE_F4
+#define RT_LDS_NODE_F4 252
+#endif
+
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -532,13 +633,21 @@ __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec
 // Lane phases of the batched state machine below.
 enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 
-template <bool kCount, bool kProf>
+template <bool kCount, bool kProf, int kWidth>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
+    constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;   // float4 per node in HBM
+    constexpr uint32_t kLdsStride = kWidth == 4 ? 7 : 4;    // float4 per node in LDS (BVH4 pad dropped)
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
+    __shared__ float4 lds_nodes[RT_LDS_NODE_F4];
     const uint32_t lane = lane_id();
     uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
+    // the top of the BVH (a breadth-first prefix) is read from LDS
+    const uint32_t lds_n = min(A.nnodes, (uint32_t)RT_LDS_NODE_F4 / kLdsStride);
+    for (uint32_t i = threadIdx.x; i < lds_n * kLdsStride; i += RT_BLOCK)
+        lds_nodes[i] = A.nodes[(i / kLdsStride) * kNodeStride + i % kLdsStride];
+    __syncthreads();
 
     // wave-uniform claim pool
     uint32_t pool_next = 0, pool_end = 0;
@@ -650,8 +759,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         mark(0);
         if (kCount && first_active()) cnt.w_iters++;
 
-        // ---- 3. closest surface hit: BVH2 traversal rounds -------------------
-        // A round = descend to a leaf (or a dead end), test the leaf, pop.  The
+        // ---- 3. closest surface hit: BVH4 traversal rounds -------------------
+        // A round = descend until every lane holds a leaf, test the leaves.  The
         // wave keeps running rounds for the lanes still searching until
         // RT_READY_BATCH lanes have their hit, then shades that batch: a lane that
         // finished early no longer holds the wave in traversal, and a lane still
@@ -661,55 +770,55 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             if (__popcll(__ballot(phase == PH_READY)) >= RT_READY_BATCH) break;
             if (phase == PH_TRAV) {
                 // the slab test needs no exact division: boxes are padded (bvh.cpp)
-                const float ix = __builtin_amdgcn_rcpf(r.d.x), iy = __builtin_amdgcn_rcpf(r.d.y),
-                            iz = __builtin_amdgcn_rcpf(r.d.z);
-                const float nox = -r.o.x * ix, noy = -r.o.y * iy, noz = -r.o.z * iz;
-                while (!(node & RT_LEAF_BIT)) {
+                const Slab sl = make_slab(r, A.tmin);
+                // Descend.  A lane that reaches a leaf postpones it and keeps
+                // descending speculatively until every lane holds a leaf or has
+                // nothing left (Aila & Laine 2009), so node steps and leaf tests
+                // both run with most lanes busy.  Culling against a not-yet-updated
+                // best_t is merely conservative.
+                uint32_t pleaf = RT_EMPTY_CHILD;
+                for (;;) {
+                  if (!(node & RT_LEAF_BIT)) {
                     if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
-                    const float4 b0 = A.nodes[node * 4 + 0];
-                    const float4 b1 = A.nodes[node * 4 + 1];
-                    const float4 b2 = A.nodes[node * 4 + 2];
-                    const float4 cf = A.nodes[node * 4 + 3];
-                    const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-                    float a0 = __builtin_fmaf(b0.x, ix, nox), a1 = __builtin_fmaf(b0.y, ix, nox);
-                    float a2 = __builtin_fmaf(b0.z, iy, noy), a3 = __builtin_fmaf(b0.w, iy, noy);
-                    float a4 = __builtin_fmaf(b1.x, iz, noz), a5 = __builtin_fmaf(b1.y, iz, noz);
-                    float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), A.tmin));
-                    float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), best_t));
-                    float e0 = __builtin_fmaf(b1.z, ix, nox), e1 = __builtin_fmaf(b1.w, ix, nox);
-                    float e2 = __builtin_fmaf(b2.x, iy, noy), e3 = __builtin_fmaf(b2.y, iy, noy);
-                    float e4 = __builtin_fmaf(b2.z, iz, noz), e5 = __builtin_fmaf(b2.w, iz, noz);
-                    float tn1 = fmaxf(fmaxf(fminf(e0, e1), fminf(e2, e3)), fmaxf(fminf(e4, e5), A.tmin));
-                    float tf1 = fminf(fminf(fmaxf(e0, e1), fmaxf(e2, e3)), fminf(fmaxf(e4, e5), best_t));
-                    bool h0 = tn0 <= tf0 && c0 != RT_EMPTY_CHILD;
-                    bool h1 = tn1 <= tf1 && c1 != RT_EMPTY_CHILD;
-                    if (h0 && h1) {
-                        uint32_t nearc = c0, farc = c1;
-                        if (tn1 < tn0) { nearc = c1; farc = c0; }
-                        stk[sp * 64] = farc;
-                        ++sp;
-                        node = nearc;
-                    } else {
-                        node = h0 ? c0 : (h1 ? c1 : RT_EMPTY_CHILD);
-                    }
+                    // flat loads: LDS for the top levels, global memory below
+                    const float4 *N = node < lds_n ? (const float4 *)&lds_nodes[node * kLdsStride]
+                                                   : A.nodes + node * kNodeStride;
+                    node = node_step<kWidth>(N, sl, best_t, stk, sp);
+                  } else if (node != RT_EMPTY_CHILD && pleaf == RT_EMPTY_CHILD) {
+                    pleaf = node;   // postpone this leaf, look for the next one
+                    node = RT_EMPTY_CHILD;
+                  }
+                  if (node == RT_EMPTY_CHILD && sp > 0) {
+                    --sp;
+                    node = stk[sp * 64];
+                  }
+                  if (__ballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD) == 0ull) break;
                 }
-                if (node != RT_EMPTY_CHILD) {
-                    const uint32_t first = RT_LEAF_FIRST(node), nleaf = RT_LEAF_COUNT(node);
-                    for (uint32_t q = 0; q < nleaf; ++q) {
+                if (pleaf != RT_EMPTY_CHILD) {
+                    const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
+                    // primitives in pairs: both 32-B heads are fetched before either test
+                    for (uint32_t q = 0; q < nleaf; q += 2) {
+                        const uint32_t ia = first + q;
+                        const bool two = q + 1 < nleaf;
+                        const uint32_t ib = two ? ia + 1 : ia;
+                        const float4 ga = A.prims[ia * 4 + 0], ma = A.prims[ia * 4 + 1];
+                        const float4 gb = A.prims[ib * 4 + 0], mb = A.prims[ib * 4 + 1];
                         int key, kind;
-                        float t = prim_t(A.prims, A.insts, first + q, r, A.tmin, key, kind);
+                        float t = prim_t_head(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
                         if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
                         if (t < best_t || (t == best_t && key < best_key)) {
-                            best_t = t; best_key = key; best_prim = first + q;
+                            best_t = t; best_key = key; best_prim = ia;
+                        }
+                        if (two) {
+                            t = prim_t_head(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
+                            if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
+                            if (t < best_t || (t == best_t && key < best_key)) {
+                                best_t = t; best_key = key; best_prim = ib;
+                            }
                         }
                     }
                 }
-                if (sp == 0) {
-                    phase = PH_READY;
-                } else {
-                    --sp;
-                    node = stk[sp * 64];
-                }
+                if (node == RT_EMPTY_CHILD) phase = PH_READY;   // stack empty too (popped above)
             }
         }
         mark(1);
@@ -723,12 +832,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            if (have) hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
+            // The media are decided first; the surface hit record is built only if
+            // no medium scatters (it is not live across the media's log()).
+            int med_mat = -1;
             for (int k = 0; k < A.nmedia; ++k) {
                 if (kCount) cnt.media++;
                 const int4 md = A.media[k];
                 float r1, r2;
-                const float4 bm = A.bprims[md.x * 4 + 3];
+                const float4 bm = A.bprims[md.x * 4 + 1];
                 if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {
                     // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
                     if (kCount) cnt.spheres++;
@@ -766,12 +877,17 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                 if (hit_distance < distance_inside_boundary) {
                     best_t = r1 + hit_distance / dlen;
                     have = true;
-                    hr.p = at(r, best_t);
-                    hr.n = mk(1, 0, 0);
-                    hr.u = 0.f;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
-                    hr.v = 0.f;
-                    hr.mat = md.w;
+                    med_mat = md.w;
                 }
+            }
+            if (med_mat >= 0) {
+                hr.p = at(r, best_t);
+                hr.n = mk(1, 0, 0);
+                hr.u = 0.f;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
+                hr.v = 0.f;
+                hr.mat = med_mat;
+            } else if (have) {
+                hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
             }
         }
 
@@ -945,14 +1061,19 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
 }  // namespace
 
 // --------------------------------------------------------------- launchers
-extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
+template <int kWidth>
+static hipError_t launch_width(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (mode == 1)
-        hipLaunchKernelGGL((rt_megakernel<true, false>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else if (mode == 2)
-        hipLaunchKernelGGL((rt_megakernel<false, true>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else
-        hipLaunchKernelGGL((rt_megakernel<false, false>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     return hipGetLastError();
+}
+
+extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
+    return a->bvh_width == 4 ? launch_width<4>(a, grid, mode, stream) : launch_width<2>(a, grid, mode, stream);
 }
 
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, const uint32_t *out_index,
@@ -962,10 +1083,15 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
     return hipGetLastError();
 }
 
-extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode) {
+template <int kWidth>
+static hipError_t occupancy_width(int *blocks_per_cu, int mode) {
     if (mode == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth>, RT_BLOCK, 0);
     if (mode == 2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth>, RT_BLOCK, 0);
+}
+
+extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width) {
+    return width == 4 ? occupancy_width<4>(blocks_per_cu, mode) : occupancy_width<2>(blocks_per_cu, mode);
 }

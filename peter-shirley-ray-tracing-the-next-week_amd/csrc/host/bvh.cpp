@@ -1,4 +1,5 @@
-// bvh.cpp — binned-SAH BVH2 over the flattened surface primitives.
+// bvh.cpp — binned-SAH BVH over the flattened surface primitives, built binary
+// and emitted breadth-first as 2-wide nodes, or collapsed into 4-wide ones.
 //
 // Replaces the reference's bvh_node construction (bvh.h:97-121: random axis,
 // median split, recursive) with a surface-area-heuristic build, and its buggy
@@ -94,12 +95,19 @@ struct Item {
     int idx;
 };
 
+// Binary node of the SAH build (emitted as rt_dnode2 / rt_dnode4 afterwards).
+struct Node2 {
+    Box box[2];
+    uint32_t ch[2];
+    int height;   // internal nodes on the longest path down, this one included
+};
+
 struct Builder {
     // SAH leaves hold at most 2 primitives: on final() that measured ~2% faster than 4 or 8
     // (tools/ab.py); RTNW_BVH_MAX_LEAF overrides (<= RT_MAX_LEAF) for experiments.
     int max_leaf = 2;
     std::vector<Item> items;
-    std::vector<rt_dnode> nodes;
+    std::vector<Node2> nodes;
     std::vector<int> order;   // leaf order -> original prim index
     int max_depth_seen = 0;
 
@@ -107,24 +115,6 @@ struct Builder {
         const uint32_t first = (uint32_t)order.size();
         for (int i = begin; i < end; i++) order.push_back(items[i].idx);
         return RT_LEAF_REF(first, end - begin);
-    }
-
-    static void put_box(rt_dnode &n, int child, const Box &b) {
-        const float lo[3] = {(float)b.lo[0], (float)b.lo[1], (float)b.lo[2]};
-        const float hi[3] = {(float)b.hi[0], (float)b.hi[1], (float)b.hi[2]};
-        // round outward so the float box contains the double box
-        float flo[3], fhi[3];
-        for (int k = 0; k < 3; k++) {
-            flo[k] = ((double)lo[k] > b.lo[k]) ? std::nextafter(lo[k], -INFINITY) : lo[k];
-            fhi[k] = ((double)hi[k] < b.hi[k]) ? std::nextafter(hi[k], INFINITY) : hi[k];
-        }
-        if (child == 0) {
-            n.b0[0] = flo[0]; n.b0[1] = fhi[0]; n.b0[2] = flo[1]; n.b0[3] = fhi[1];
-            n.b1[0] = flo[2]; n.b1[1] = fhi[2];
-        } else {
-            n.b1[2] = flo[0]; n.b1[3] = fhi[0];
-            n.b2[0] = flo[1]; n.b2[1] = fhi[1]; n.b2[2] = flo[2]; n.b2[3] = fhi[2];
-        }
     }
 
     Box range_box(int begin, int end) const {
@@ -219,19 +209,122 @@ struct Builder {
             return leaf(begin, end);
         }
         const uint32_t id = (uint32_t)nodes.size();
-        nodes.push_back(rt_dnode{});
+        nodes.push_back(Node2{});
         max_depth_seen = std::max(max_depth_seen, depth + 1);
         if (depth + 1 > RT_MAX_BVH_DEPTH) throw std::runtime_error("bvh: depth budget exceeded");
         const Box lb = range_box(begin, s), rb = range_box(s, end);
         const uint32_t l = build(begin, s, depth + 1);
         const uint32_t r = build(s, end, depth + 1);
-        rt_dnode &n = nodes[id];
-        put_box(n, 0, lb);
-        put_box(n, 1, rb);
+        Node2 &n = nodes[id];
+        n.box[0] = lb;
+        n.box[1] = rb;
         n.ch[0] = l;
         n.ch[1] = r;
-        n.ch[2] = n.ch[3] = 0;
+        n.height = 1 + std::max(height(l), height(r));
         return id;
+    }
+
+    int height(uint32_t ref) const { return (ref & RT_LEAF_BIT) ? 0 : nodes[ref].height; }
+};
+
+// Child `c`'s box rounded outward to float.
+void float_box(const Box &b, float lo[3], float hi[3]) {
+    for (int a = 0; a < 3; a++) {
+        const float l = (float)b.lo[a], h = (float)b.hi[a];
+        lo[a] = ((double)l > b.lo[a]) ? std::nextafter(l, -INFINITY) : l;
+        hi[a] = ((double)h < b.hi[a]) ? std::nextafter(h, INFINITY) : h;
+    }
+}
+void put_box(rt_dnode4 &n, int c, const Box &b) {
+    float lo[3], hi[3];
+    float_box(b, lo, hi);
+    for (int a = 0; a < 3; a++) {
+        float *q = n.q[2 * a + (c >> 1)] + 2 * (c & 1);
+        q[0] = lo[a];
+        q[1] = hi[a];
+    }
+}
+void put_box(rt_dnode2 &n, int c, const Box &b) {
+    float lo[3], hi[3];
+    float_box(b, lo, hi);
+    float *f = &n.b[0][0] + 6 * c;   // (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z) of child c
+    for (int a = 0; a < 3; a++) {
+        f[2 * a] = lo[a];
+        f[2 * a + 1] = hi[a];
+    }
+}
+
+// Emits the binary tree breadth-first, 2-wide as built or collapsed 4-wide: a
+// node opens its largest-area interior child into that child's two children
+// until it has `width`.  `budget`
+// bounds the traversal stack below the node: a node with n children pushes at
+// most n-1 of them, so a child may be opened only while (n-1) + the tallest
+// remaining binary subtree (its own worst case) still fits.
+template <class Node>
+struct Collapser {
+    const Builder &b;
+    int width;
+    std::vector<Node> out;
+
+    struct Cand { uint32_t ref; Box box; };
+
+    // Children of one 4-wide node (n of them) for binary node `ref`.
+    int expand(uint32_t ref, int budget, Cand cs[4]) const {
+        const Node2 &n2 = b.nodes[ref];
+        cs[0] = {n2.ch[0], n2.box[0]};
+        cs[1] = {n2.ch[1], n2.box[1]};
+        int n = 2;
+        auto bound = [&](int skip, int extra_height, int count) {
+            int h = extra_height;
+            for (int i = 0; i < n; i++) if (i != skip) h = std::max(h, b.height(cs[i].ref));
+            return count - 1 + h;
+        };
+        while (n < width) {
+            int best = -1;
+            double best_area = -1;
+            for (int i = 0; i < n; i++) {
+                if (cs[i].ref & RT_LEAF_BIT) continue;
+                const Node2 &c = b.nodes[cs[i].ref];
+                const int h = std::max(b.height(c.ch[0]), b.height(c.ch[1]));
+                if (bound(i, h, n + 1) > budget) continue;
+                const double area = cs[i].box.area();
+                if (area > best_area) { best_area = area; best = i; }
+            }
+            if (best < 0) break;
+            const Node2 &c = b.nodes[cs[best].ref];
+            const Cand a = {c.ch[0], c.box[0]}, d = {c.ch[1], c.box[1]};
+            cs[best] = a;
+            cs[n++] = d;
+        }
+        return n;
+    }
+
+    // Nodes are numbered breadth-first, so the top levels are a prefix of the
+    // array (the device keeps that prefix in LDS).
+    uint32_t collapse(uint32_t root, int budget) {
+        struct Job { uint32_t ref; int budget; uint32_t id; };
+        std::vector<Job> queue;
+        out.push_back(Node{});
+        queue.push_back({root, budget, 0});
+        for (size_t qi = 0; qi < queue.size(); ++qi) {
+            const Job j = queue[qi];
+            Cand cs[4];
+            const int n = expand(j.ref, j.budget, cs);
+            uint32_t ch[4] = {RT_EMPTY_CHILD, RT_EMPTY_CHILD, RT_EMPTY_CHILD, RT_EMPTY_CHILD};
+            for (int i = 0; i < n; i++) {
+                if (cs[i].ref & RT_LEAF_BIT) {
+                    ch[i] = cs[i].ref;
+                } else {
+                    ch[i] = (uint32_t)out.size();
+                    out.push_back(Node{});
+                    queue.push_back({cs[i].ref, j.budget - (n - 1), ch[i]});
+                }
+            }
+            Node &node = out[j.id];
+            for (int i = 0; i < n; i++) put_box(node, i, cs[i].box);
+            for (int i = 0; i < 4; i++) node.ch[i] = ch[i];
+        }
+        return 0;
     }
 };
 
@@ -250,20 +343,29 @@ BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, f
         for (int k = 0; k < 3; k++) it.c[k] = 0.5 * (it.box.lo[k] + it.box.hi[k]);
         it.idx = i;
     }
-    const uint32_t root = b.build(0, n, 0);
-    if (root & RT_LEAF_BIT) {   // tiny scene: wrap the single leaf in a root node
-        rt_dnode r{};
-        Builder::put_box(r, 0, b.range_box(0, n));
-        r.ch[0] = root;
-        r.ch[1] = RT_EMPTY_CHILD;
-        b.nodes.push_back(r);
-        res.root = (uint32_t)b.nodes.size() - 1;
-        res.depth = 1;
-    } else {
+    int width = 2;
+    if (const char *e = std::getenv("RTNW_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
+    res.width = width;
+    const uint32_t root2 = b.build(0, n, 0);
+    auto emit = [&](auto &out_nodes, auto node_tag) {
+        using Node = decltype(node_tag);
+        Collapser<Node> c{b, width, {}};
+        if (root2 & RT_LEAF_BIT) {   // tiny scene: wrap the single leaf in a root node
+            Node r{};
+            put_box(r, 0, b.range_box(0, n));
+            r.ch[0] = root2;
+            r.ch[1] = r.ch[2] = r.ch[3] = RT_EMPTY_CHILD;
+            c.out.push_back(r);
+            res.depth = 1;
+        } else {
+            c.collapse(root2, RT_STACK_DEPTH - 1);
+            res.depth = b.max_depth_seen;
+        }
         res.root = 0;
-        res.depth = b.max_depth_seen;
-    }
-    res.nodes = std::move(b.nodes);
+        out_nodes = std::move(c.out);
+    };
+    if (width == 4) emit(res.nodes4, rt_dnode4{});
+    else emit(res.nodes2, rt_dnode2{});
     res.order = std::move(b.order);
     return res;
 }

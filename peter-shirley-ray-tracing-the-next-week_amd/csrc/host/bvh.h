@@ -9,13 +9,16 @@
 namespace rtnw {
 
 struct BvhResult {
-    std::vector<rt_dnode> nodes;
+    int width = 2;                 // 2: rt_dnode2, 4: rt_dnode4 (rt_layout.h)
+    std::vector<rt_dnode2> nodes2;
+    std::vector<rt_dnode4> nodes4;
     std::vector<int> order;   // leaf order -> index into the input primitives
     uint32_t root = 0;
-    int depth = 0;            // internal nodes on the longest root-to-leaf path
+    int depth = 0;            // binary-build internal nodes on the longest root-to-leaf path
 };
 
 // Primitive boxes cover moving spheres over [min(0, time0), max(0, time1)].
+// width: 2 or 4 (RTNW_BVH_WIDTH overrides).
 BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, float time0, float time1);
 
 }  // namespace rtnw

@@ -61,13 +61,12 @@ rt_dprim to_dprim(const rt_prim &p, int order) {
         d.g1[0] = q[3] - q[0]; d.g1[1] = q[4] - q[1]; d.g1[2] = q[5] - q[2]; d.g1[3] = q[6];
         d.g2[0] = q[7] - q[6];
         break;
-    default:   // rects
+    default:   // rects (k goes to m[1])
         d.g0[0] = q[0]; d.g0[1] = q[1]; d.g0[2] = q[2]; d.g0[3] = q[3];
-        d.g1[0] = q[4];
         break;
     }
-    d.m[0] = p.kind | (p.flip ? 1 << 8 : 0);
-    d.m[1] = p.material;
+    d.m[0] = p.kind | (p.flip ? 1 << 8 : 0) | (p.material << 9);
+    d.m[1] = p.kind >= RT_PRIM_XY_RECT ? ibits(q[4]) : 0;   // rect plane k
     d.m[2] = p.instance;
     d.m[3] = order;
     return d;
@@ -75,13 +74,13 @@ rt_dprim to_dprim(const rt_prim &p, int order) {
 
 // SURVEY §8d byte model (bytes the algorithm must read or write, independent of
 // this implementation's record padding):
-//   BVH2 node fetch 64 B (two child boxes + refs); sphere 16 B; moving sphere 36 B;
+//   node fetch: the bytes loaded per visit (BVH2 64 B, BVH4 112 B); sphere 16 B; moving sphere 36 B;
 //   rect 24 B; instance chain entered 32 B; medium record 16 B; material +
 //   texture per shade 16 + 16 B; Perlin turbulence 7 octaves x 8 gradient gathers
 //   x (12 B gradient + 3 x 4 B permutation) = 1344 B; per work item the 16-B
 //   partial sum written and read back; 12 B of output per pixel.
-double algorithmic_bytes(const rt_stats &st, double items, double pixels) {
-    return 64.0 * st.node_visits + 16.0 * st.sphere_tests + 36.0 * st.moving_sphere_tests + 24.0 * st.rect_tests +
+double algorithmic_bytes(const rt_stats &st, double items, double pixels, int bvh_width) {
+    return (bvh_width == 4 ? 112.0 : 64.0) * st.node_visits + 16.0 * st.sphere_tests + 36.0 * st.moving_sphere_tests + 24.0 * st.rect_tests +
            32.0 * st.instanced_tests + 16.0 * st.medium_tests + 32.0 * st.shades + 1344.0 * st.noise_evals +
            32.0 * items + 12.0 * pixels;
 }
@@ -97,7 +96,7 @@ struct rt_scene {
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
          *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr;
     uint32_t root = 0;
-    int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0;
+    int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2;
     bool has_moving = false;
     float time0 = 0, time1 = 1;
     // job cache
@@ -154,6 +153,7 @@ static int validate_desc(const rt_scene_desc *d) {
     if (d->nprims < 0 || d->nboundary < 0 || d->nmedia < 0 || d->nmaterials < 0 || d->ntextures < 0 || d->ninstances < 0)
         return fail(RT_ERR_INVALID, "negative count in scene descriptor");
     if (d->nprims > (1 << 24) - 1 || d->nboundary > (1 << 24) - 1) return fail(RT_ERR_INVALID, "too many primitives");
+    if (d->nmaterials > (1 << 22)) return fail(RT_ERR_INVALID, "too many materials");
     if (!d->perlin_ranvec || !d->perlin_perm) return fail(RT_ERR_INVALID, "missing Perlin tables");
     if (d->nimages < 0 || d->image_bytes < 0 || (d->nimages > 0 && (!d->images || !d->image_data)))
         return fail(RT_ERR_INVALID, "bad image arrays");
@@ -324,7 +324,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     for (int v : perm) if (v < 0 || v > 255) return cleanup(fail(RT_ERR_INVALID, "Perlin permutation entry out of range"));
 
     int rc;
-    if ((rc = upload(&s->nodes, bvh.nodes)) || (rc = upload(&s->prims, prims)) || (rc = upload(&s->bprims, bprims)) ||
+    if ((rc = bvh.width == 4 ? upload(&s->nodes, bvh.nodes4) : upload(&s->nodes, bvh.nodes2)) || (rc = upload(&s->prims, prims)) || (rc = upload(&s->bprims, bprims)) ||
         (rc = upload(&s->media, media)) || (rc = upload(&s->mats, mats)) || (rc = upload(&s->texs, texs)) ||
         (rc = upload(&s->insts, insts)) || (rc = upload(&s->ranvec, ranvec)) || (rc = upload(&s->perm, perm)) ||
         (rc = upload(&s->texels, texels)))
@@ -333,7 +333,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->has_bvh = d->nprims > 0;
     s->nmedia = d->nmedia;
     s->bvh_depth = bvh.depth;
-    s->nnodes = (int)bvh.nodes.size();
+    s->nnodes = (int)(bvh.width == 4 ? bvh.nodes4.size() : bvh.nodes2.size());
+    s->bvh_width = bvh.width;
     s->nprims = d->nprims;
 
     hipDeviceProp_t prop;
@@ -341,7 +342,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->cus = prop.multiProcessorCount;
     for (int mode = 0; mode < 3; mode++) {
         int bpc = 0;
-        if ((e = rt_megakernel_occupancy(&bpc, mode)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+        if ((e = rt_megakernel_occupancy(&bpc, mode, s->bvh_width)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+        // RTNW_BLOCKS_PER_CU caps the resident workgroups per CU (occupancy experiments only)
+        if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) bpc = std::min(bpc, std::max(1, std::atoi(e)));
         s->grid[mode] = std::max(1, bpc) * s->cus;
     }
     if ((e = hipMalloc(&s->counter, 64)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc counter"));
@@ -430,6 +433,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.perm = (const int *)s->perm;
     a.texels = (const uint8_t *)s->texels;
     a.root = s->root;
+    a.nnodes = (uint32_t)s->nnodes;
+    a.bvh_width = s->bvh_width;
     a.has_bvh = s->has_bvh;
     a.nmedia = s->nmedia;
     for (int k = 0; k < 3; k++) {
@@ -489,7 +494,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->medium_tests = (double)c[RT_CNT_MEDIA];
             stats->shades = (double)c[RT_CNT_SHADES];
             stats->noise_evals = (double)c[RT_CNT_NOISE];
-            stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, (double)s->npix);
+            stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, (double)s->npix, s->bvh_width);
             unsigned long long w[5];
             HIP_TRY(hipMemcpy(w, (unsigned long long *)s->stats + RT_CNT_N + 4, sizeof w, hipMemcpyDeviceToHost));
             stats->wave_iterations = (double)w[0];

@@ -24,25 +24,46 @@
 #define RT_LEAF_FIRST(ref) ((ref) & 0x00FFFFFFu)
 #define RT_LEAF_COUNT(ref) ((((ref) >> 24) & 0x7Fu) + 1)
 
+// The BVH comes in two widths (RTNW_BVH_WIDTH, default 2), nodes numbered
+// breadth-first so the top levels are a prefix of the array (kept in LDS).
+//
 // BVH2 node, 64 B: the boxes of BOTH children, so one node fetch decides which
-// children to enter.  b0..b2 hold the boxes as
+// children to enter:
 //   b0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
 //   b1 = (c0.lo.z, c0.hi.z, c1.lo.x, c1.hi.x)
 //   b2 = (c1.lo.y, c1.hi.y, c1.lo.z, c1.hi.z)
 //   ch = (child0, child1, -, -)
-struct rt_dnode {
-    float b0[4], b1[4], b2[4];
+struct rt_dnode2 {
+    float b[3][4];
     uint32_t ch[4];
 };
 
-// Primitive, 64 B.  g0..g2 by kind:
+// BVH4 node, 128 B: the boxes of up to four children.  Each axis interval is a
+// (lo, hi) pair and a float4 holds the pairs of two children, so one packed FMA
+// yields both slab distances of a pair:
+//   q[0] = x of c0, c1   q[1] = x of c2, c3
+//   q[2] = y of c0, c1   q[3] = y of c2, c3
+//   q[4] = z of c0, c1   q[5] = z of c2, c3      each (lo, hi, lo, hi)
+//   ch   = child references (RT_EMPTY_CHILD: unused slot)
+//   pad  = keeps nodes on 128-B lines; never read
+// Builder guarantee (both widths): along any root-to-leaf path the children
+// beyond the first sum to <= RT_STACK_DEPTH - 1, which bounds the traversal stack.
+struct rt_dnode4 {
+    float q[6][4];
+    uint32_t ch[4];
+    uint32_t pad[4];
+};
+
+// Primitive, 64 B, ordered so the first 32 B (g0, m) are all a sphere or rect test
+// reads; only a moving sphere reads the whole record.  g0..g2 by kind:
 //   sphere:        g0 = (cx, cy, cz, r)
 //   moving sphere: g0 = (c0x, c0y, c0z, r), g1 = (c1x-c0x, c1y-c0y, c1z-c0z, t0), g2 = (t1-t0, ...)
-//   rects:         g0 = (a0, a1, b0, b1), g1 = (k, ...)
-// m = (kind | flip << 8, material, instance (-1 none), list order)
+//   rects:         g0 = (a0, a1, b0, b1)
+// m = (kind | flip << 8 | material << 9, rect k (float bits), instance (-1 none), list order)
 struct rt_dprim {
-    float g0[4], g1[4], g2[4];
+    float g0[4];
     int32_t m[4];
+    float g1[4], g2[4];
 };
 
 // Material, 32 B: (kind, texture, fuzz, ref_idx) + (albedo.xyz, flags)

@@ -45,6 +45,17 @@ for step in "$@"; do
             run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
             run pmc_l2 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
             run pmc_sq 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmc_deep) export TMPDIR=/tmp
+            B="python3 bench.py --spp ${PMC_SPP:-128} --steps 1 --warmup 0 --no-cpu-baseline"
+            run pmc_d2 600 rocprofv3 --pmc TA_TA_BUSY GRBM_GUI_ACTIVE -d gpurun_out/pmc_d2 -o run --output-format csv -- $B
+            run pmc_d3 600 rocprofv3 --pmc TD_TD_BUSY -d gpurun_out/pmc_d3 -o run --output-format csv -- $B
+            run pmc_d4 600 rocprofv3 --pmc TA_FLAT_READ_WAVEFRONTS -d gpurun_out/pmc_d4 -o run --output-format csv -- $B
+            run pmc_d5 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES -d gpurun_out/pmc_d5 -o run --output-format csv -- $B
+            run pmc_d6 600 rocprofv3 --pmc TCP_CACHE_MISS -d gpurun_out/pmc_d6 -o run --output-format csv -- $B
+            run pmc_d7 600 rocprofv3 --pmc TCP_PENDING_STALL_CYCLES -d gpurun_out/pmc_d7 -o run --output-format csv -- $B
+            run pmc_d8 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_FLAT SQ_WAIT_ANY SQ_WAIT_INST_ANY -d gpurun_out/pmc_d8 -o run --output-format csv -- $B
+            run pmc_d9 600 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU -d gpurun_out/pmc_d9 -o run --output-format csv -- $B
+            python3 tools/pmc_deep.py gpurun_out > gpurun_out/pmc_deep.txt ;;
     ab)     run ab 1200 python3 tools/ab.py $AB_LIBS --rounds ${AB_ROUNDS:-2} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
