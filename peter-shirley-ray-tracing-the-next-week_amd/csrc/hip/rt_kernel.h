@@ -4,7 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define RT_BLOCK 256   // 4 waves per workgroup
+#define RT_BLOCK 256      // 4 waves per workgroup
+#define RT_WF_SLOTS 512   // path slots per workgroup of the wavefront engine
 
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)
@@ -40,10 +41,20 @@ struct RtKernelArgs {
     float4 *slab;             // [nchunks][npix] partial sums
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)
+    // wavefront engine path state (rt_wavefront.hip), grid x RT_WF_SLOTS records each
+    float4 *wf_ray_o;   // origin, time
+    float4 *wf_ray_d;   // direction, -
+    float2 *wf_hit;     // closest t, primitive (bits; ~0 none)
+    float4 *wf_beta;    // throughput, depth (int bits)
+    float4 *wf_part;    // the work item's running sum
+    uint4 *wf_rng;      // sample stream counter, medium key
+    uint4 *wf_samp;     // work item, next sample, end sample, -
 };
 
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
+extern "C" hipError_t rt_launch_wavefront(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);
+extern "C" hipError_t rt_wavefront_occupancy(int *blocks_per_cu, int mode, int width);
 // mode: 0 plain, 1 count, 2 profile; width: BVH width of the scene (2 or 4)
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);

@@ -27,587 +27,9 @@
 // Arithmetic follows the reference's float/double promotions; the file is compiled
 // with -ffp-contract=off so no FMA is introduced where the reference has none (the
 // BVH slab test, which decides nothing about the result, uses explicit fmaf).
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "rt_layout.h"
-#include "rt_kernel.h"
-
-#define RT_FLT_MAX 0x1.fffffep+127f
-#define RT_INF __builtin_huge_valf()
+#include "rt_device.h"
 
 namespace {
-
-// ------------------------------------------------------------------ vec3
-struct V3 { float x, y, z; };
-__device__ __forceinline__ V3 mk(float a, float b, float c) { V3 r; r.x = a; r.y = b; r.z = c; return r; }
-__device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ V3 scale(float t, V3 v) { return mk(t * v.x, t * v.y, t * v.z); }
-__device__ __forceinline__ V3 divs(V3 v, float t) { return mk(v.x / t, v.y / t, v.z / t); }
-__device__ __forceinline__ V3 neg(V3 v) { return mk(-v.x, -v.y, -v.z); }
-__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ float len(V3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
-__device__ __forceinline__ V3 unit(V3 v) { return divs(v, len(v)); }
-__device__ __forceinline__ float comp(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
-
-struct Ray { V3 o, d; float time; };
-__device__ __forceinline__ V3 at(const Ray &r, float t) { return add(r.o, scale(t, r.d)); }
-
-// ------------------------------------------------------------------- RNG
-// Counter streams: sample (pixel, s) draws u48(mix64(key + n*GAMMA)),
-// n = 1, 2, ...; constant_medium k at bounce b draws from a second keyed stream.
-constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-__device__ __forceinline__ double u48(uint64_t z) { return (double)(z >> 16) * 0x1p-48; }
-__device__ __forceinline__ uint64_t sample_key(uint64_t seed, uint32_t pixel, uint32_t sample) {
-    return mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) ^ (((uint64_t)pixel << 32) | sample));
-}
-struct Rng {
-    uint64_t ctr;    // key + n*GAMMA for the last draw n (n = 0 after start)
-    uint64_t mkey;   // medium stream key, derived once per sample
-    __device__ __forceinline__ void start(uint64_t k) { ctr = k; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
-    __device__ __forceinline__ double next() { ctr += kGamma; return u48(mix64(ctr)); }
-    __device__ __forceinline__ double medium(int bounce, int k) const {
-        uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
-        return u48(mix64(mkey + (m + 1) * kGamma));
-    }
-};
-
-// pow(x, 5.0) for the x = (double)(float) of schlick (material.h:19).  x has 24
-// significant bits, so x*x is exact; x^4 and x^5 are carried as double-double and
-// rounded once: the double result is the correctly rounded x^5 except in
-// vanishingly rare near-ties, i.e. what glibc's pow returns, at a fraction of
-// ocml's general pow cost (and register pressure).
-__device__ __forceinline__ double pow5(double x) {
-    const double x2 = x * x;
-    const double x4h = x2 * x2;
-    const double x4l = __builtin_fma(x2, x2, -x4h);
-    const double p = x4h * x;
-    const double pe = __builtin_fma(x4h, x, -p);
-    return p + (pe + x4l * x);
-}
-
-// ----------------------------------------------------------- scene access
-__device__ __forceinline__ float4 ld4(const float4 *p, uint32_t i) { return p[i]; }
-__device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
-
-// BVH slab test primitives.  Packed FP32 FMA for the lo/hi plane pairs; min/max
-// as plain VALU ops: their operands are never signalling NaNs (FMA results, t_min,
-// the current best t), so the IEEE-mode quieting the compiler would add per use
-// of a loop-carried value is dead weight.  (minnum semantics: a NaN plane distance
-// from an axis-parallel ray leaves that axis unconstrained, i.e. conservative.)
-typedef float F2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ F2 pk_fma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ float vmin(float a, float b) {
-    float r;
-    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ float vmax(float a, float b) {
-    float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ float vmin3(float a, float b, float c) {
-    float r;
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
-// Ray into the object space of an instance chain (hitable.h:66-67, 129-135).
-__device__ __forceinline__ Ray to_object(const float4 *insts, int inst, Ray r) {
-    const float4 *I = insts + inst * 7;
-    int nops = fbits(I[0].x);
-    for (int k = 0; k < nops; ++k) {
-        float4 op = I[1 + k];
-        int code = fbits(op.x);
-        if (code == RT_OP_TRANSLATE) {
-            r.o = sub(r.o, mk(op.y, op.z, op.w));
-        } else if (code == RT_OP_ROTATE_Y) {
-            float s = op.y, c = op.z;
-            V3 o = r.o, d = r.d;
-            o.x = c * r.o.x - s * r.o.z;
-            o.z = s * r.o.x + c * r.o.z;
-            d.x = c * r.d.x - s * r.d.z;
-            d.z = s * r.d.x + c * r.d.z;
-            r.o = o; r.d = d;
-        }
-    }
-    return r;
-}
-
-// Hit point / normal back to world space, innermost wrapper first (hitable.h:43-45, 69, 137-145).
-__device__ __forceinline__ void to_world(const float4 *insts, int inst, V3 &p, V3 &n) {
-    const float4 *I = insts + inst * 7;
-    int nops = fbits(I[0].x);
-    for (int k = nops - 1; k >= 0; --k) {
-        float4 op = I[1 + k];
-        int code = fbits(op.x);
-        if (code == RT_OP_TRANSLATE) {
-            p = add(p, mk(op.y, op.z, op.w));
-        } else if (code == RT_OP_ROTATE_Y) {
-            float s = op.y, c = op.z;
-            V3 q = p, m = n;
-            q.x = c * p.x + s * p.z;
-            q.z = -s * p.x + c * p.z;
-            m.x = c * n.x + s * n.z;
-            m.z = -s * n.x + c * n.z;
-            p = q; n = m;
-        } else if (code == RT_OP_FLIP) {
-            n = neg(n);
-        }
-    }
-}
-
-// Candidate hit distance of one primitive for a search starting at t_min with no
-// upper bound (RT_INF = miss).  The caller keeps the closest (t, key) pair, which
-// reproduces hitable_list's sequential `t < closest` / `t <= closest` acceptance.
-__device__ __forceinline__ float sphere_t(V3 c, float rad, const Ray &r, float tmin) {   // sphere.h:25-52
-    V3 oc = sub(r.o, c);
-    float a = dot(r.d, r.d);
-    float b = dot(oc, r.d);
-    float cc = dot(oc, oc) - rad * rad;
-    float disc = b * b - a * cc;
-    if (disc > 0) {
-        float t = (-b - sqrtf(disc)) / a;
-        if (t < RT_FLT_MAX && t > tmin) return t;
-        t = (-b + sqrtf(disc)) / a;
-        if (t < RT_FLT_MAX && t > tmin) return t;
-    }
-    return RT_INF;
-}
-
-__device__ __forceinline__ V3 msphere_center(float4 g0, float4 g1, float4 g2, float time) {   // sphere.h:81-83
-    return add(mk(g0.x, g0.y, g0.z), scale((time - g1.w) / g2.x, mk(g1.x, g1.y, g1.z)));
-}
-
-// One rect test for a plane axis (aarect.h:50-100); oa/da: ray along the plane
-// normal, (oi, di) and (oj, dj): the two in-plane axes.  Written once per kind
-// with direct field reads so the compiler never indexes the ray through memory.
-__device__ __forceinline__ float plane_t(float oa, float da, float oi, float di, float oj, float dj, float4 g0, float k,
-                                         float tmin) {
-    float t = (k - oa) / da;
-    if (t < tmin || t > RT_FLT_MAX) return RT_INF;
-    float a = oi + t * di;
-    float b = oj + t * dj;
-    if (a < g0.x || a > g0.y || b < g0.z || b > g0.w) return RT_INF;
-    return t;
-}
-__device__ __forceinline__ float rect_t(int kind, float4 g0, float k, const Ray &r, float tmin) {
-    if (kind == RT_PRIM_XY_RECT) return plane_t(r.o.z, r.d.z, r.o.x, r.d.x, r.o.y, r.d.y, g0, k, tmin);
-    if (kind == RT_PRIM_XZ_RECT) return plane_t(r.o.y, r.d.y, r.o.x, r.d.x, r.o.z, r.d.z, g0, k, tmin);
-    return plane_t(r.o.x, r.d.x, r.o.y, r.d.y, r.o.z, r.d.z, g0, k, tmin);
-}
-
-// prim kinds: 0 sphere, 1 moving sphere, 2 xy, 3 xz, 4 yz  (rect axis = 2, 1, 0)
-__device__ __forceinline__ int rect_axis(int kind) { return 4 - kind; }
-
-// Test of one primitive whose 32-B head (g0, mm) is already loaded.
-__device__ __forceinline__ float prim_t_head(float4 g0, float4 mm, const float4 *P, const float4 *insts, uint32_t idx,
-                                             const Ray &r0, float tmin, int &key, int &kind_out) {
-    int kind = fbits(mm.x) & 0xff;
-    int inst = fbits(mm.z);
-    int order = fbits(mm.w);
-    kind_out = kind | (inst >= 0 ? 0x100 : 0);
-    Ray r = r0;
-    if (inst >= 0) r = to_object(insts, inst, r0);
-    float t;
-    if (kind == RT_PRIM_SPHERE) {
-        t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, r, tmin);
-        key = order;
-    } else if (kind == RT_PRIM_MOVING_SPHERE) {
-        t = sphere_t(msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time), g0.w, r, tmin);
-        key = order;
-    } else {
-        t = rect_t(kind, g0, mm.y, r, tmin);
-        key = -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
-    }
-    return t;
-}
-
-__device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float tmin,
-                                        int &key, int &kind_out) {
-    return prim_t_head(P[idx * 4 + 0], P[idx * 4 + 1], P, insts, idx, r0, tmin, key, kind_out);
-}
-
-struct Hit { V3 p, n; float u, v; int mat; };
-
-// get_sphere_uv (hitable.h:14-19): float atan2/asin, then the double M_PI arithmetic.
-__device__ __forceinline__ void sphere_uv(V3 p, float &u, float &v) {
-    const float phi = atan2f(p.z, p.x);
-    const float theta = asinf(p.y);
-    u = (float)(1 - ((double)phi + 3.14159265358979323846) / (2 * 3.14159265358979323846));
-    v = (float)(((double)theta + 3.14159265358979323846 / 2) / 3.14159265358979323846);
-}
-
-// Rebuilds the reference's hit_record for the winning primitive (sphere.h:34-38,
-// 103-106; aarect.h:58-63; hitable.h:43-45, 69, 137-145).
-// (u, v) is computed only for materials whose texture reads it (an image texture):
-// every other texture ignores it (texture.h:22-56).
-__device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts, const float4 *mats, uint32_t idx,
-                                           const Ray &r0, float t) {
-    const float4 g0 = P[idx * 4 + 0];
-    const float4 mm = P[idx * 4 + 1];
-    int kind = fbits(mm.x) & 0xff;
-    int flip = (fbits(mm.x) >> 8) & 1;
-    int inst = fbits(mm.z);
-    Ray r = r0;
-    if (inst >= 0) r = to_object(insts, inst, r0);
-    Hit h;
-    h.p = at(r, t);
-    if (kind == RT_PRIM_SPHERE) {
-        h.n = divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w);
-    } else if (kind == RT_PRIM_MOVING_SPHERE) {
-        h.n = divs(sub(h.p, msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time)), g0.w);
-    } else {
-        int axis = rect_axis(kind);
-        h.n = mk(axis == 0 ? 1.f : 0.f, axis == 1 ? 1.f : 0.f, axis == 2 ? 1.f : 0.f);
-    }
-    h.u = 0.f;
-    h.v = 0.f;
-    h.mat = fbits(mm.x) >> 9;
-    if (fbits(mats[h.mat * 2 + 1].w) & 1) {
-        if (kind == RT_PRIM_SPHERE) {
-            sphere_uv(divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w), h.u, h.v);   // sphere.h:36
-        } else if (kind != RT_PRIM_MOVING_SPHERE) {                          // aarect.h:54-59
-            float oi, di, oj, dj;
-            if (kind == RT_PRIM_XY_RECT) { oi = r.o.x; di = r.d.x; oj = r.o.y; dj = r.d.y; }
-            else if (kind == RT_PRIM_XZ_RECT) { oi = r.o.x; di = r.d.x; oj = r.o.z; dj = r.d.z; }
-            else { oi = r.o.y; di = r.d.y; oj = r.o.z; dj = r.d.z; }
-            const float a = oi + t * di, b = oj + t * dj;
-            h.u = (a - g0.x) / (g0.y - g0.x);
-            h.v = (b - g0.z) / (g0.w - g0.z);
-        }
-    }
-    if (flip) h.n = neg(h.n);
-    if (inst >= 0) to_world(insts, inst, h.p, h.n);
-    return h;
-}
-
-// Closest boundary hit of a constant_medium (its own small list), t > / >= tmin.
-__device__ __forceinline__ uint32_t lanes_below(uint64_t mask);
-// true on exactly one active lane: counts a wave-level event once per wave
-__device__ __forceinline__ bool first_active() { return lanes_below(__ballot(1)) == 0; }
-
-struct Counters {
-    uint64_t samples = 0, segments = 0, nodes = 0, spheres = 0, mspheres = 0, rects = 0, instanced = 0, media = 0,
-             shades = 0, noise = 0;
-    // wave-level trip counts (SIMD efficiency = lane-level count / (64 x wave-level count))
-    uint64_t w_iters = 0, w_nodes = 0, w_prims = 0, w_rius = 0, l_rius = 0;
-    __device__ __forceinline__ void prim(int kind) {
-        const int k = kind & 0xff;
-        if (k == RT_PRIM_SPHERE) spheres++;
-        else if (k == RT_PRIM_MOVING_SPHERE) mspheres++;
-        else rects++;
-        if (kind & 0x100) instanced++;
-    }
-};
-
-template <bool kCount>
-__device__ __forceinline__ float boundary_t(const float4 *B, const float4 *insts, int first, int count, const Ray &r,
-                                            float tmin, Counters &cnt) {
-    float best = RT_INF;
-    for (int q = 0; q < count; ++q) {
-        int key, kind;
-        float t = prim_t(B, insts, (uint32_t)(first + q), r, tmin, key, kind);
-        if (kCount) cnt.prim(kind);
-        if (t < best) best = t;
-    }
-    return best;
-}
-
-// ----------------------------------------------------------------- Perlin
-// One noise() (perlin.h:43-61, 25-39).  The six permutation reads are issued
-// together, then the eight gradient reads: two memory round trips per call.
-__device__ __forceinline__ float perlin_noise(const float4 *ranvec, const int *perm, V3 p) {
-    float u = p.x - floorf(p.x);
-    float v = p.y - floorf(p.y);
-    float w = p.z - floorf(p.z);
-    u = u * u * (3 - 2 * u);
-    v = v * v * (3 - 2 * v);
-    w = w * w * (3 - 2 * w);
-    const int i = (int)floorf(p.x);
-    const int j = (int)floorf(p.y);
-    const int k = (int)floorf(p.z);
-    const float uu = u * u * (3 - 2 * u);
-    const float vv = v * v * (3 - 2 * v);
-    const float ww = w * w * (3 - 2 * w);
-    const int px[2] = {perm[i & 255], perm[(i + 1) & 255]};
-    const int py[2] = {perm[256 + (j & 255)], perm[256 + ((j + 1) & 255)]};
-    const int pz[2] = {perm[512 + (k & 255)], perm[512 + ((k + 1) & 255)]};
-    float accum = 0;   // corner order i, j, k as perlin_interp sums them
-#pragma unroll 1
-    for (int a = 0; a < 2; ++a) {
-        V3 g[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float4 t = ranvec[px[a] ^ py[c >> 1] ^ pz[c & 1]];
-            g[c] = mk(t.x, t.y, t.z);
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int b = c >> 1, d = c & 1;
-            V3 weight_v = mk(u - a, v - b, w - d);
-            accum += (a * uu + (1 - a) * (1 - uu)) * (b * vv + (1 - b) * (1 - vv)) * (d * ww + (1 - d) * (1 - ww)) *
-                     dot(g[c], weight_v);
-        }
-    }
-    return accum;
-}
-
-// Texture chain of one lane down to its leaf: checker_texture picks a child by
-// the sign of the sines (texture.h:35-44).  Returns the leaf kind (-1: chain too deep).
-__device__ __forceinline__ int tex_leaf(const RtKernelArgs &A, int ti, V3 p, float4 &t0, float4 &t1) {
-    for (int guard = 0; guard < RT_MAX_CHECKER_DEPTH; ++guard) {
-        t0 = A.texs[ti * 2 + 0];
-        t1 = A.texs[ti * 2 + 1];
-        const int kind = fbits(t0.x);
-        if (kind != RT_TEX_CHECKER) return kind;
-        float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
-        ti = (sines < 0) ? fbits(t0.z) : fbits(t0.y);
-    }
-    return -1;
-}
-
-// texture::value of a constant or image leaf (texture.h:16-27; surface_texture.h:19-30);
-// the noise leaf is finished after coop_turb.
-__device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, float4 t0, float4 t1, float u, float v) {
-    if (kind == RT_TEX_CONSTANT) return mk(t1.x, t1.y, t1.z);
-    if (kind == RT_TEX_IMAGE) {   // stride 3 as the reference addresses it
-        const int nx = fbits(t0.y), ny = fbits(t0.z);
-        const uint8_t *data = A.texels + fbits(t0.w);
-        int i = (int)((1 - u) * nx);
-        int j = (int)((double)((1 - v) * ny) - 0.001);
-        if (i < 0) i = 0;
-        if (j < 0) j = 0;
-        if (i > nx - 1) i = nx - 1;
-        if (j > ny - 1) j = ny - 1;
-        const float r = (float)((int)data[3 * i + 3 * nx * j] / 255.0);
-        const float gg = (float)((int)data[3 * i + 3 * nx * j + 1] / 255.0);
-        const float b = (float)((int)data[3 * i + 3 * nx * j + 2] / 255.0);
-        return mk(r, gg, b);
-    }
-    return mk(0, 0, 0);
-}
-
-// ------------------------------------------------------------ BVH node step
-// Per-ray slab-test constants: 1/d (padded boxes need no exact division) and
-// -o/d, duplicated into packed pairs for v_pk_fma_f32.
-struct Slab { F2 ix, iy, iz, nox, noy, noz; float tmin; };
-__device__ __forceinline__ Slab make_slab(const Ray &r, float tmin) {
-    const float ix = __builtin_amdgcn_rcpf(r.d.x), iy = __builtin_amdgcn_rcpf(r.d.y), iz = __builtin_amdgcn_rcpf(r.d.z);
-    Slab s;
-    s.ix = F2{ix, ix}; s.iy = F2{iy, iy}; s.iz = F2{iz, iz};
-    s.nox = F2{-r.o.x * ix, -r.o.x * ix}; s.noy = F2{-r.o.y * iy, -r.o.y * iy}; s.noz = F2{-r.o.z * iz, -r.o.z * iz};
-    s.tmin = tmin;
-    return s;
-}
-// entry distance of one child box, +inf if the ray misses it (or the slot is empty)
-__device__ __forceinline__ float box_entry(const Slab &s, F2 x, F2 y, F2 z, float best_t, uint32_t c) {
-    const F2 a = pk_fma(x, s.ix, s.nox), b = pk_fma(y, s.iy, s.noy), e = pk_fma(z, s.iz, s.noz);
-    const float tn = vmax3(vmin(a.x, a.y), vmin(b.x, b.y), vmax(vmin(e.x, e.y), s.tmin));
-    const float tf = vmin3(vmax(a.x, a.y), vmax(b.x, b.y), vmin(vmax(e.x, e.y), best_t));
-    return (tn <= tf && c != RT_EMPTY_CHILD) ? tn : RT_INF;
-}
-__device__ __forceinline__ void cas(float &ka, uint32_t &ca, float &kb, uint32_t &cb) {
-    const bool sw = kb < ka;
-    const float tk = sw ? kb : ka;
-    kb = sw ? ka : kb;
-    ka = tk;
-    const uint32_t tc = sw ? cb : ca;
-    cb = sw ? ca : cb;
-    ca = tc;
-}
-// One interior node: test the children, push the hit ones but the nearest far to
-// near (branch-free: a slot is written, then kept only if the child was hit; the
-// builder bounds sp by RT_STACK_DEPTH - 1), return the nearest (or empty).
-template <int kWidth>
-__device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, float best_t, uint32_t *stk, int &sp) {
-    if (kWidth == 2) {   // rt_dnode2
-        const float4 b0 = N[0], b1 = N[1], b2 = N[2], cf = N[3];
-        const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-        const float k0 = box_entry(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, c0);
-        const float k1 = box_entry(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, c1);
-        const bool second = k1 < k0;   // ties: child 0 first
-        const uint32_t nearc = second ? c1 : c0, farc = second ? c0 : c1;
-        const float kn = second ? k1 : k0, kf = second ? k0 : k1;
-        stk[sp * 64] = farc;
-        sp += kf != RT_INF;
-        return kn != RT_INF ? nearc : RT_EMPTY_CHILD;
-    } else {             // rt_dnode4
-        const float4 qx01 = N[0], qx23 = N[1], qy01 = N[2], qy23 = N[3], qz01 = N[4], qz23 = N[5], cf = N[6];
-        uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y), c2 = (uint32_t)fbits(cf.z),
-                 c3 = (uint32_t)fbits(cf.w);
-        float k0 = box_entry(s, F2{qx01.x, qx01.y}, F2{qy01.x, qy01.y}, F2{qz01.x, qz01.y}, best_t, c0);
-        float k1 = box_entry(s, F2{qx01.z, qx01.w}, F2{qy01.z, qy01.w}, F2{qz01.z, qz01.w}, best_t, c1);
-        float k2 = box_entry(s, F2{qx23.x, qx23.y}, F2{qy23.x, qy23.y}, F2{qz23.x, qz23.y}, best_t, c2);
-        float k3 = box_entry(s, F2{qx23.z, qx23.w}, F2{qy23.z, qy23.w}, F2{qz23.z, qz23.w}, best_t, c3);
-        cas(k0, c0, k1, c1);   // sorting network, nearest first
-        cas(k2, c2, k3, c3);
-        cas(k0, c0, k2, c2);
-        cas(k1, c1, k3, c3);
-        cas(k1, c1, k2, c2);
-        stk[sp * 64] = c3;
-        sp += k3 != RT_INF;
-        stk[sp * 64] = c2;
-        sp += k2 != RT_INF;
-        stk[sp * 64] = c1;
-        sp += k1 != RT_INF;
-        return k0 != RT_INF ? c0 : RT_EMPTY_CHILD;
-    }
-}
-
-// --------------------------------------------------------------- scatter
-// Candidates of the two rejection loops: `base` is the stream counter before the
-// candidate's first draw.
-struct SphereCand {   // material.h:41-47 random_in_unit_sphere
-    __device__ __forceinline__ bool operator()(uint64_t base, V3 &p) const {
-        const double x = u48(mix64(base + kGamma)), y = u48(mix64(base + 2 * kGamma)), z = u48(mix64(base + 3 * kGamma));
-        p = sub(scale(2.0f, mk((float)x, (float)y, (float)z)), mk(1, 1, 1));
-        return (double)dot(p, p) < 1.0;
-    }
-};
-struct DiskCand {     // camera.h:6-12 random_in_unit_disk
-    __device__ __forceinline__ bool operator()(uint64_t base, V3 &p) const {
-        const double a = u48(mix64(base + kGamma)), b = u48(mix64(base + 2 * kGamma));
-        p = sub(scale(2.0f, mk((float)a, (float)b, 0)), mk(1, 1, 0));
-        return (double)dot(p, p) < 1.0;
-    }
-};
-__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, scale(2 * dot(v, n), n)); }   // material.h:36-38
-
-// ------------------------------------------------------------ work claim
-__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
-__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
-
-// ------------------------------------------- cooperative rejection sampling
-// The rejection loops of the reference (camera.h:6-12 random_in_unit_disk,
-// material.h:41-47 random_in_unit_sphere) accept the first candidate inside the
-// unit ball; candidate c of a loop entered after draw n uses draws n+K*c+1 ..
-// n+K*c+K.  Counter streams are random access, so the wave evaluates the
-// candidates of all lanes that need a point at once: the m requesting lanes
-// publish (stream position) in LDS slots 0..m-1 and all 64 lanes take candidates
-// round-robin (lane L evaluates candidate c0 + L/m of slot L%m).  Each owner keeps
-// its lowest accepted candidate, so the point and the draws consumed are exactly
-// those of its own sequential loop; rounds repeat for owners whose candidates all
-// failed.  A lane loop that ran ~6 wave trips at ~16% SIMD efficiency (the
-// slowest lane of 48 decides) takes ~2-3 fully used trips.
-// Must be called with all 64 lanes of the wave active.
-struct CoopSlot {
-    uint64_t ctr;
-    uint64_t pad;
-};
-
-template <int K, bool kCount, class Cand>
-__device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt, Cand cand) {
-    V3 res = mk(0, 0, 0);
-    bool pending = want;
-    uint64_t U = __ballot(pending);
-    while (U != 0ull) {
-        const uint32_t m = (uint32_t)__popcll(U);            // wave-uniform
-        uint64_t P = 0;                                        // lanes congruent to 0 mod m
-        for (uint32_t b = 0; b < 64; b += m) P |= 1ull << b;
-        const uint32_t r = lanes_below(U);
-        if (pending) slots[r].ctr = g.ctr;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // t = lane / m exactly: lane < 64, m <= 64, inv = ceil(2^16 / m)
-        const uint32_t inv = (0xFFFFu + m) / m;
-        const uint32_t t = (lane * inv) >> 16;
-        const uint32_t slot = lane - t * m;
-        const uint64_t base = slots[slot].ctr + (uint64_t)(K * t) * kGamma;
-        V3 p;
-        const bool ok = cand(base, p);
-        const uint64_t okm = __ballot(ok);
-        if (kCount && first_active()) cnt.w_rius++;
-        uint32_t src = lane;
-        bool won = false;
-        if (pending) {
-            const uint64_t mine = P << r;
-            const uint64_t win = okm & mine;
-            if (win != 0ull) {
-                src = (uint32_t)__builtin_ctzll(win);
-                const uint32_t tried = (uint32_t)__popcll(mine & ((1ull << src) - 1ull)) + 1u;
-                g.ctr += (uint64_t)(K * tried) * kGamma;
-                if (kCount) cnt.l_rius += tried;
-                won = true;
-                pending = false;
-            } else {
-                const uint32_t tried = (uint32_t)__popcll(mine);
-                g.ctr += (uint64_t)(K * tried) * kGamma;
-                if (kCount) cnt.l_rius += tried;
-            }
-        }
-        // every lane takes part in the exchange (bpermute reads the source lane's register)
-        const float px = __shfl(p.x, (int)src), py = __shfl(p.y, (int)src), pz = __shfl(p.z, (int)src);
-        if (won) res = mk(px, py, pz);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        U = __ballot(pending);
-    }
-    return res;
-}
-
-// Cooperative turbulence (perlin.h:64-74).  Octave k of turb(q) is
-// noise(q * 2^k) weighted 2^-k: `temp_p *= 2` and `weight *= 0.5` are exact, so
-// the octaves are independent.  The lanes that need turb publish q in LDS and the
-// wave evaluates the 7 octaves of up to 9 of them at once, one noise() per lane;
-// each owner gathers its 7 values and sums them in octave order, exactly as the
-// reference's loop does.  A wave with one noisy lane used to run all 7 octaves as
-// a chain of 28 dependent gathers; now it runs one noise() per round.
-// Must be called with all 64 lanes of the wave active.
-__device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec, const int *perm, CoopSlot *slots,
-                                           uint32_t lane) {
-    const uint64_t U = __ballot(want);
-    if (U == 0ull) return 0.f;
-    float res = 0.f;
-    const uint32_t m = (uint32_t)__popcll(U);
-    const uint32_t r = lanes_below(U);
-    float4 *pts = reinterpret_cast<float4 *>(slots);
-    if (want) pts[r] = make_float4(q.x, q.y, q.z, 0.f);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t lo = lane / 7, oct = lane - lo * 7;
-    for (uint32_t base = 0; base < m; base += 9) {
-        const uint32_t o = base + lo;
-        float val = 0.f;
-        if (lane < 63 && o < m) {
-            const float4 pt = pts[o];
-            const float s = (float)(1u << oct);
-            val = perlin_noise(ranvec, perm, mk(pt.x * s, pt.y * s, pt.z * s));
-        }
-        const bool mine = want && r >= base && r < base + 9;
-        const uint32_t src0 = ((r - base) * 7u) & 63u;
-        float acc = 0.f, weight = 1.0f;
-#pragma unroll
-        for (int kk = 0; kk < 7; ++kk) {
-            const float nk = __shfl(val, (int)((src0 + kk) & 63u));
-            acc += weight * nk;
-            weight = (float)((double)weight * 0.5);
-        }
-        if (mine) res = fabsf(acc);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    return res;
-}
 
 // Minimum waves per SIMD the register allocation must allow (launch_bounds second
 // argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  Traversal is latency-bound, so
@@ -618,10 +40,10 @@ __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec
 #define RT_READY_BATCH 48
 #endif
 
-// float4 of BVH nodes kept in LDS per workgroup: 252 x 16 B fills the LDS left by
-// 4 workgroups per CU (stacks 32 KB + sampler slots 4 KB each): 63 BVH2 or 36 BVH4 nodes.
+// float4 of BVH nodes kept in LDS per workgroup: 508 x 16 B fills the LDS left by
+// 4 workgroups per CU (stacks 24 KB + sampler slots 4 KB each): 127 BVH2 or 72 BVH4 nodes.
 #ifndef RT_LDS_NODE_F4
-#define RT_LDS_NODE_F4 252
+#define RT_LDS_NODE_F4 508
 #endif
 
 #ifndef RT_WAVES_PER_SIMD
@@ -826,66 +248,17 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         // Stages 4-5 keep the whole wave active (the cooperative sampler needs it).
         const bool ready = phase == PH_READY;
 
-        // ---- 4. media after the surfaces (constant_medium.h:26-50) -------------
+        // ---- 4. media after the surfaces, then the hit record -------------------
         bool have = false;
         Hit hr;
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            // The media are decided first; the surface hit record is built only if
-            // no medium scatters (it is not live across the media's log()).
-            int med_mat = -1;
-            for (int k = 0; k < A.nmedia; ++k) {
-                if (kCount) cnt.media++;
-                const int4 md = A.media[k];
-                float r1, r2;
-                const float4 bm = A.bprims[md.x * 4 + 1];
-                if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {
-                    // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
-                    if (kCount) cnt.spheres++;
-                    const float4 sg = A.bprims[md.x * 4 + 0];
-                    V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
-                    float a = dot(r.d, r.d);
-                    float b = dot(oc, r.d);
-                    float cc = dot(oc, oc) - sg.w * sg.w;
-                    float disc = b * b - a * cc;
-                    if (!(disc > 0)) continue;
-                    const float ta = (-b - sqrtf(disc)) / a;
-                    const float tb = (-b + sqrtf(disc)) / a;
-                    if (ta < RT_FLT_MAX && ta > -RT_FLT_MAX) r1 = ta;
-                    else if (tb < RT_FLT_MAX && tb > -RT_FLT_MAX) r1 = tb;
-                    else continue;
-                    const float tmin2 = (float)((double)r1 + 0.0001);
-                    if (ta < RT_FLT_MAX && ta > tmin2) r2 = ta;
-                    else if (tb < RT_FLT_MAX && tb > tmin2) r2 = tb;
-                    else continue;
-                } else {
-                    r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
-                    if (r1 == RT_INF) continue;
-                    r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
-                    if (r2 == RT_INF) continue;
-                }
-                float tmax = have ? best_t : RT_FLT_MAX;
-                if (r1 < A.tmin) r1 = A.tmin;
-                if (r2 > tmax) r2 = tmax;
-                if (r1 >= r2) continue;
-                if (r1 < 0) r1 = 0;
-                float dlen = len(r.d);
-                float distance_inside_boundary = (r2 - r1) * dlen;
-                float density = __int_as_float(md.z);
-                float hit_distance = (float)((double)(-(1 / density)) * log(g.medium(depth, k)));
-                if (hit_distance < distance_inside_boundary) {
-                    best_t = r1 + hit_distance / dlen;
-                    have = true;
-                    med_mat = md.w;
-                }
-            }
+            const int med_mat = media_hit<kCount>(A, r, depth, g, have, best_t, cnt);
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);
-                hr.u = 0.f;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
-                hr.v = 0.f;
-                hr.mat = med_mat;
+                hr.mat = med_mat;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
             } else if (have) {
                 hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
             }
@@ -893,122 +266,15 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
 
         mark(2);
         // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
-        // The per-material work that dominates (texture lookup, the rejection loop
-        // of random_in_unit_sphere) runs ONCE for every lane that needs it instead
-        // of once per material branch; each lane still makes exactly the draws its
-        // own material makes, in the same order (one material per lane).
-        const bool shading = ready && have;
-        int kind = -1;
-        bool live = false, noisy = false;
-        float nscale = 0.f;
-        V3 tv = mk(0, 0, 0);
-        if (shading) {
-            if (kCount) cnt.shades++;
-            kind = fbits(A.mats[hr.mat * 2 + 0].x);
-            live = depth < A.max_depth;
-            const bool textured = kind == RT_MAT_DIFFUSE_LIGHT ||
-                                  (live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC));
-            if (textured) {
-                float4 t0, t1;
-                const int tkind = tex_leaf(A, fbits(A.mats[hr.mat * 2 + 0].y), hr.p, t0, t1);   // texture.h:35-44
-                noisy = tkind == RT_TEX_NOISE;
-                nscale = t0.w;
-                if (!noisy) tv = tex_value_leaf(A, tkind, t0, t1, hr.u, hr.v);
-            }
-        }
-        if (kCount && noisy) cnt.noise++;
-        const float turb = coop_turb(noisy, scale(nscale, hr.p), A.ranvec, A.perm, slots, lane);   // perlin.h:64-74
-        if (noisy) {                                                                               // texture.h:52-56
-            const float sv = 1 + sinf(nscale * hr.p.x + 5 * turb);
-            const float h = 0.5f * 1;
-            tv = mk(sv * h, sv * h, sv * h);
-        }
-        const bool wants_sphere = shading && live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_METAL ||
-                                                      kind == RT_MAT_ISOTROPIC);
-        const V3 rius = coop_reject<3, kCount>(wants_sphere, g, slots, lane, cnt, SphereCand());   // material.h:41-47
+        const ShadeOut so = shade<kCount>(A, ready, have, r, hr, depth, g, slots, lane, cnt);
         if (ready) {
-            V3 L;
-            bool terminate = true;
-            if (!have) {
-                if (A.background == RT_BG_SKY) {                                  // TNW/Chapter03:29-31
-                    V3 ud = unit(r.d);
-                    float t = (float)(0.5 * ((double)ud.y + 1.0));
-                    V3 sky = add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
-                    L = mul(beta, sky);
-                } else {
-                    L = mul(beta, mk(0, 0, 0));
-                }
+            if (so.scattered) {
+                beta = mul(beta, so.att);
+                r = so.ray;
+                ++depth;
+                begin_segment();
             } else {
-                const float4 m0 = A.mats[hr.mat * 2 + 0];
-                const float4 m1 = A.mats[hr.mat * 2 + 1];
-                V3 emitted = kind == RT_MAT_DIFFUSE_LIGHT ? tv : mk(0, 0, 0);
-                bool scattered = false;
-                V3 att = mk(0, 0, 0);
-                Ray ns;
-                if (live) {
-                    if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
-                        V3 target = add(add(hr.p, hr.n), rius);
-                        ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
-                        att = tv;
-                        scattered = true;
-                    } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
-                        V3 reflected = reflect(unit(r.d), hr.n);
-                        ns.o = hr.p; ns.d = add(reflected, scale(m0.z, rius)); ns.time = 0.0f;
-                        att = mk(m1.x, m1.y, m1.z);
-                        scattered = dot(ns.d, hr.n) > 0;
-                    } else if (kind == RT_MAT_DIELECTRIC) {                       // material.h:90-120
-                        const float ref_idx = m0.w;
-                        V3 outward_normal;
-                        V3 reflected = reflect(r.d, hr.n);
-                        float ni_over_nt, cosine;
-                        att = mk(1.0f, 1.0f, 1.0f);
-                        float dn = dot(r.d, hr.n);
-                        if (dn > 0) {
-                            outward_normal = neg(hr.n);
-                            ni_over_nt = ref_idx;
-                            cosine = dot(r.d, hr.n) / len(r.d);
-                            cosine = sqrtf(1 - ref_idx * ref_idx * (1 - cosine * cosine));
-                        } else {
-                            outward_normal = hr.n;
-                            ni_over_nt = (float)(1.0 / (double)ref_idx);
-                            cosine = -dot(r.d, hr.n) / len(r.d);
-                        }
-                        // refract, material.h:23-33
-                        V3 uv = unit(r.d);
-                        float dt = dot(uv, outward_normal);
-                        float disc = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
-                        float reflect_prob;
-                        V3 refracted = mk(0, 0, 0);
-                        if (disc > 0) {
-                            refracted = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))),
-                                            scale(sqrtf(disc), outward_normal));
-                            // schlick, material.h:16-20
-                            float r0 = (1 - ref_idx) / (1 + ref_idx);
-                            r0 = r0 * r0;
-                            reflect_prob = (float)(r0 + (double)(1 - r0) * pow5((double)(1 - cosine)));
-                        } else {
-                            reflect_prob = 1.0f;
-                        }
-                        ns.o = hr.p; ns.time = 0.0f;
-                        ns.d = (g.next() < (double)reflect_prob) ? reflected : refracted;
-                        scattered = true;
-                    } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
-                        ns.o = hr.p; ns.d = rius; ns.time = 0.0f;
-                        att = tv;
-                        scattered = true;
-                    }
-                }
-                if (scattered) {
-                    beta = mul(beta, att);
-                    r = ns;
-                    ++depth;
-                    terminate = false;
-                    begin_segment();
-                } else {
-                    L = mul(beta, emitted);
-                }
-            }
-            if (terminate) {
+                V3 L = mul(beta, so.emitted);
                 if (!(L.x == L.x)) L.x = 0;                                       // de_nan, main.cpp:232-242
                 if (!(L.y == L.y)) L.y = 0;
                 if (!(L.z == L.z)) L.z = 0;

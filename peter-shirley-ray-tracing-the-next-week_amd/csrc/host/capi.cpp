@@ -90,7 +90,8 @@ double algorithmic_bytes(const rt_stats &st, double items, double pixels, int bv
 struct rt_scene {
     int device = 0;
     int cus = 0;
-    int grid[3] = {0, 0, 0};   // persistent grid per kernel variant (plain, count, profile)
+    int grid[3] = {0, 0, 0};      // persistent megakernel grid per variant (plain, count, profile)
+    int grid_wf[3] = {0, 0, 0};   // persistent wavefront-engine grid per variant
     hipStream_t own_stream = nullptr;
     // scene in HBM
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
@@ -106,6 +107,8 @@ struct rt_scene {
     void *slab = nullptr;
     size_t slab_bytes = 0;
     void *counter = nullptr, *stats = nullptr;
+    void *wf = nullptr;           // wavefront-engine path state (grid x RT_WF_SLOTS records)
+    size_t wf_bytes = 0;
     void *host_out = nullptr;
     size_t host_out_bytes = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -220,7 +223,7 @@ static int validate_desc(const rt_scene_desc *d) {
 void rt_scene_destroy(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    for (void *p : {s->nodes, s->prims, s->bprims, s->media, s->mats, s->texs, s->insts, s->ranvec, s->perm, s->texels, s->job_xy,
+    for (void *p : {s->wf, s->nodes, s->prims, s->bprims, s->media, s->mats, s->texs, s->insts, s->ranvec, s->perm, s->texels, s->job_xy,
                     s->job_out, s->slab, s->counter, s->stats, s->host_out})
         if (p) (void)hipFree(p);
     for (auto &e : s->ev) if (e) (void)hipEventDestroy(e);
@@ -346,6 +349,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         // RTNW_BLOCKS_PER_CU caps the resident workgroups per CU (occupancy experiments only)
         if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) bpc = std::min(bpc, std::max(1, std::atoi(e)));
         s->grid[mode] = std::max(1, bpc) * s->cus;
+        int wbpc = 0;
+        if ((e = rt_wavefront_occupancy(&wbpc, mode == 2 ? 0 : mode, s->bvh_width)) != hipSuccess)
+            return cleanup(hip_fail(e, "occupancy query"));
+        if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) wbpc = std::min(wbpc, std::max(1, std::atoi(e)));
+        s->grid_wf[mode] = std::max(1, wbpc) * s->cus;
     }
     if ((e = hipMalloc(&s->counter, 64)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc counter"));
     if ((e = hipMalloc(&s->stats, (RT_CNT_N + 16) * sizeof(unsigned long long))) != hipSuccess)
@@ -465,9 +473,34 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.counter = (uint32_t *)s->counter;
     a.stats = (unsigned long long *)s->stats;
 
+    // engine: the megakernel (default) or the workgroup wavefront (RTNW_ENGINE=wave,
+    // rt_wavefront.hip; no profile variant: a profile request runs it plain)
+    const char *eng = std::getenv("RTNW_ENGINE");
+    const bool wave = eng && std::strcmp(eng, "wave") == 0;
+    if (wave) {
+        const size_t nslots = (size_t)s->grid_wf[mode] * RT_WF_SLOTS;
+        const size_t need = nslots * (5 * sizeof(float4) + sizeof(float2) + sizeof(uint4));
+        if (need > s->wf_bytes) {
+            if (s->wf) (void)hipFree(s->wf);
+            s->wf = nullptr;
+            s->wf_bytes = 0;
+            HIP_TRY(hipMalloc(&s->wf, need));
+            s->wf_bytes = need;
+        }
+        char *w = (char *)s->wf;
+        a.wf_ray_o = (float4 *)w; w += nslots * sizeof(float4);
+        a.wf_ray_d = (float4 *)w; w += nslots * sizeof(float4);
+        a.wf_beta = (float4 *)w; w += nslots * sizeof(float4);
+        a.wf_part = (float4 *)w; w += nslots * sizeof(float4);
+        a.wf_rng = (uint4 *)w; w += nslots * sizeof(uint4);
+        a.wf_samp = (uint4 *)w; w += nslots * sizeof(uint4);
+        a.wf_hit = (float2 *)w;
+    }
+
     const float k = (float)(1.0 / (double)(float)p->spp);   // vec3::operator/= (vec3.h:134-141)
     HIP_TRY(hipEventRecord(s->ev[0], stream));
-    HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
+    if (wave) HIP_TRY(rt_launch_wavefront(&a, s->grid_wf[mode], mode == 2 ? 0 : mode, stream));
+    else HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
     HIP_TRY(hipEventRecord(s->ev[1], stream));
     HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, nchunks, k, (const uint32_t *)s->job_out, out_dev, stream));
     HIP_TRY(hipEventRecord(s->ev[2], stream));
@@ -511,7 +544,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->cycles_media = (double)c[RT_CNT_N + 2];
             stats->cycles_shade = (double)c[RT_CNT_N + 3];
         }
-        stats->grid = (double)s->grid[mode];
+        stats->grid = (double)(wave ? s->grid_wf[mode] : s->grid[mode]);
     }
     return RT_OK;
 }

@@ -11,8 +11,9 @@
 
 #include "rt_hip.h"   // enum values (prim / material / texture kinds, ops)
 
-#define RT_STACK_DEPTH 32          // traversal stack entries per lane (LDS)
-#define RT_MAX_BVH_DEPTH 31        // builder guarantee: a root-to-leaf path has <= 31 internal nodes
+#define RT_STACK_DEPTH 24          // traversal stack entries per lane (LDS)
+#define RT_MAX_BVH_DEPTH 23        // builder guarantee: a root-to-leaf path has <= 23 internal nodes
+                                   // (a median split of 2^24 - 1 primitives, the ABI maximum, fits)
 #define RT_MAX_LEAF 8              // primitives per leaf
 #define RT_MAX_INSTANCE_OPS 6
 #define RT_MAX_CHECKER_DEPTH 16
