@@ -5,7 +5,7 @@
 #include <stdint.h>
 
 #define RT_BLOCK 256      // 4 waves per workgroup
-#define RT_WF_SLOTS 512   // path slots per workgroup of the wavefront engine
+#define RT_WF_SLOTS 1024  // path slots per workgroup of the wavefront engine
 
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)

@@ -4,21 +4,22 @@
 // shared device code is rt_device.h), organised differently.  A persistent
 // workgroup owns RT_WF_SLOTS camera paths whose state lives in HBM (SoA, one
 // record per slot; the working set of a workgroup is ~50 KB and stays in L2 /
-// MALL).  The workgroup runs three compacted phases in turn, separated by
-// workgroup barriers:
+// MALL).  Each wave owns a quarter of the slots and runs three compacted phases
+// on them in turn, with wave-local lists and no workgroup barriers (a wave in the
+// tail of a phase idles only its own lanes; the SIMD's other waves keep issuing):
 //
 //   C  camera   slots whose path ended: retire / claim work items, draw the next
 //               camera sample (camera.h:41-56) -> ray
-//   T  trace    slots with a ray: closest hit through the BVH; each wave fetches
-//               rays from the workgroup's list as its lanes finish, so lanes stay
-//               busy until the list runs dry (persistent while-while)
+//   T  trace    slots with a ray: closest hit through the BVH; lanes fetch the
+//               next ray of the wave's list as they finish, so they stay busy
+//               until the list runs dry (persistent while-while)
 //   S  shade    slots with a hit: media, hit record, material scatter -> the
 //               next ray, or the path's radiance added to the item's sum
 //
 // In the megakernel every stage runs inside one wave whose lanes are at
 // different stages, so each stage executes with only part of the wave active
 // and all path state is live in registers across all of them.  Here each phase
-// runs its own code over a compacted list with whole waves, and only that
+// runs its own code over a compacted list with the whole wave, and only that
 // phase's registers are live.
 //
 // Determinism and parity are those of the megakernel: a slot processes its work
@@ -32,63 +33,82 @@
 
 namespace {
 
-constexpr int kWfSlots = RT_WF_SLOTS;               // path slots per workgroup
-constexpr int kSlotsPerThread = kWfSlots / RT_BLOCK;
-static_assert(kWfSlots % RT_BLOCK == 0, "slots per workgroup must be a multiple of the block size");
+constexpr int kWfSlots = RT_WF_SLOTS;                   // path slots per workgroup
+constexpr int kWaveSlots = kWfSlots / (RT_BLOCK / 64);   // ... per wave
+static_assert(kWaveSlots % 64 == 0, "slots per wave must be a multiple of 64");
 
 enum : uint32_t { ST_EMPTY = 0, ST_CAMERA = 1, ST_TRACE = 2, ST_HIT = 3 };
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-// Appends the slots of one status to the workgroup's list (any order: slots are
-// independent).  Returns the list length; all threads must call it.
-__device__ __forceinline__ uint32_t build_list(const uint8_t *status, uint32_t want, uint16_t *list, uint32_t *count,
-                                               uint32_t lane) {
-    if (threadIdx.x == 0) *count = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kSlotsPerThread; ++k) {
-        const uint32_t slot = threadIdx.x + k * RT_BLOCK;
-        const bool mine = status[slot] == want;
-        const uint64_t m = __ballot(mine);
-        uint32_t base = 0;
-        if (lane == 0 && m) base = atomicAdd(count, (uint32_t)__popcll(m));
-        base = __shfl(base, 0);
-        if (mine) list[base + lanes_below(m)] = (uint16_t)slot;
-    }
-    __syncthreads();
-    return *count;
+// Orders this wave's LDS writes before its later LDS reads by other lanes.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool kCount, int kWidth>
+// The wave's slots of one status, compacted into `list` (slot order); returns
+// the count (wave-uniform).
+__device__ __forceinline__ uint32_t build_list(const uint8_t *status, uint32_t want, uint16_t *list, uint32_t lane) {
+    wave_sync();
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < kWaveSlots / 64; ++k) {
+        const uint32_t slot = k * 64 + lane;
+        const bool mine = status[slot] == want;
+        const uint64_t m = __ballot(mine);
+        if (mine) list[n + lanes_below(m)] = (uint16_t)slot;
+        n += (uint32_t)__popcll(m);
+    }
+    wave_sync();
+    return n;
+}
+
+// kProf: wave-level s_memtime per phase (RT_FLAG_PROFILE; stats cycles_claim =
+// phase C, cycles_traverse = phase T, cycles_media = phase S, cycles_shade =
+// list building).  Diagnostic only.
+template <bool kCount, bool kProf, int kWidth>
 __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(RtKernelArgs A) {
     constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
-    __shared__ uint16_t list[kWfSlots];
-    __shared__ uint8_t status[kWfSlots];
-    __shared__ uint32_t list_n, list_next;
+    __shared__ uint16_t lds_list[RT_BLOCK / 64][kWaveSlots];
+    __shared__ uint8_t lds_status[RT_BLOCK / 64][kWaveSlots];
 
     const uint32_t lane = lane_id();
     uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
-    const size_t sbase = (size_t)blockIdx.x * kWfSlots;
+    uint16_t *list = lds_list[threadIdx.x >> 6];
+    uint8_t *status = lds_status[threadIdx.x >> 6];
+    const size_t sbase = (size_t)blockIdx.x * kWfSlots + (threadIdx.x >> 6) * kWaveSlots;
     Counters cnt;
+    uint64_t prof[4] = {0, 0, 0, 0};
+    uint64_t stamp = kProf ? __builtin_amdgcn_s_memtime() : 0;
+    auto mark = [&](int k) {
+        if (kProf) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            prof[k] += now - stamp;
+            stamp = now;
+        }
+    };
 
     // wave-uniform work-item pool (one global atomic per 64 items)
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
 
-    for (int k = 0; k < kSlotsPerThread; ++k) {
-        const uint32_t slot = threadIdx.x + k * RT_BLOCK;
+    for (int k = 0; k < kWaveSlots / 64; ++k) {
+        const uint32_t slot = k * 64 + lane;
         status[slot] = ST_CAMERA;
         A.wf_samp[sbase + slot] = make_uint4(kNone, 0, 0, 0);   // item, s_cur, s_end, -
     }
 
     for (;;) {
         // ---- C: retire finished items, claim new ones, camera samples -------------
-        const uint32_t nc = build_list(status, ST_CAMERA, list, &list_n, lane);
-        for (uint32_t b = 0; b < nc; b += RT_BLOCK) {   // workgroup-uniform trip count
-            const uint32_t i = b + threadIdx.x;
+        mark(3);
+        const uint32_t nc = build_list(status, ST_CAMERA, list, lane);
+        mark(3);
+        for (uint32_t b = 0; b < nc; b += 64) {
+            const uint32_t i = b + lane;
             const uint32_t slot = i < nc ? list[i] : 0;
             const size_t gs = sbase + slot;
             uint4 sm = make_uint4(kNone, 0, 0, 0);
@@ -166,15 +186,15 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 if (kCount) { cnt.samples++; cnt.segments++; }
             }
         }
-        __syncthreads();
+        mark(0);
 
         // ---- T: closest surface hits -------------------------------------------
-        const uint32_t nt = build_list(status, ST_TRACE, list, &list_n, lane);
-        if (nt == 0) break;   // every slot is empty: the job is done
-        if (threadIdx.x == 0) list_next = 0;
-        __syncthreads();
+        const uint32_t nt = build_list(status, ST_TRACE, list, lane);
+        if (nt == 0) break;   // every slot of the wave is empty: its share of the job is done
+        mark(3);
         {
             uint32_t slot = kNone;
+            uint32_t next = 0;   // wave-uniform position in the list
             bool dry = false;
             Ray r;
             r.o = mk(0, 0, 0); r.d = mk(0, 0, 0); r.time = 0;
@@ -189,9 +209,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 const bool idle = slot == kNone;
                 const uint64_t idle_mask = __ballot(idle);
                 if (idle_mask != 0ull && !dry) {
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(&list_next, (uint32_t)__popcll(idle_mask));
-                    base = __shfl(base, 0);
+                    const uint32_t base = next;
+                    next += (uint32_t)__popcll(idle_mask);
                     if (base >= nt) dry = true;
                     const uint32_t idx = base + lanes_below(idle_mask);
                     if (idle && idx < nt) {
@@ -259,12 +278,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 }
             }
         }
-        __syncthreads();
+        mark(1);
 
         // ---- S: media, hit record, material scatter ----------------------------
-        const uint32_t ns = build_list(status, ST_HIT, list, &list_n, lane);
-        for (uint32_t b = 0; b < ns; b += RT_BLOCK) {
-            const uint32_t i = b + threadIdx.x;
+        const uint32_t ns = build_list(status, ST_HIT, list, lane);
+        mark(3);
+        for (uint32_t b = 0; b < ns; b += 64) {
+            const uint32_t i = b + lane;
             const bool ready = i < ns;
             const uint32_t slot = ready ? list[i] : 0;
             const size_t gi = sbase + slot;
@@ -332,8 +352,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 }
             }
         }
-        __syncthreads();
+        mark(2);
     }
+    if (kProf && lane == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_CNT_N + k], (unsigned long long)prof[k]);
 
     if (kCount) {
         uint64_t v[RT_CNT_N] = {cnt.samples, cnt.segments, cnt.nodes, cnt.spheres, cnt.mspheres, cnt.rects,
@@ -351,9 +373,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
 template <int kWidth>
 static hipError_t wf_launch_width(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (mode == 1)
-        hipLaunchKernelGGL((rt_wavefront<true, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_wavefront<true, false, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+    else if (mode == 2)
+        hipLaunchKernelGGL((rt_wavefront<false, true, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else
-        hipLaunchKernelGGL((rt_wavefront<false, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_wavefront<false, false, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     return hipGetLastError();
 }
 
@@ -364,8 +388,10 @@ extern "C" hipError_t rt_launch_wavefront(const RtKernelArgs *a, int grid, int m
 template <int kWidth>
 static hipError_t wf_occupancy_width(int *blocks_per_cu, int mode) {
     if (mode == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_wavefront<true, kWidth>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_wavefront<false, kWidth>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_wavefront<true, false, kWidth>, RT_BLOCK, 0);
+    if (mode == 2)
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_wavefront<false, true, kWidth>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_wavefront<false, false, kWidth>, RT_BLOCK, 0);
 }
 
 extern "C" hipError_t rt_wavefront_occupancy(int *blocks_per_cu, int mode, int width) {

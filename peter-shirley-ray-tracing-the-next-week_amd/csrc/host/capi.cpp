@@ -350,7 +350,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) bpc = std::min(bpc, std::max(1, std::atoi(e)));
         s->grid[mode] = std::max(1, bpc) * s->cus;
         int wbpc = 0;
-        if ((e = rt_wavefront_occupancy(&wbpc, mode == 2 ? 0 : mode, s->bvh_width)) != hipSuccess)
+        if ((e = rt_wavefront_occupancy(&wbpc, mode, s->bvh_width)) != hipSuccess)
             return cleanup(hip_fail(e, "occupancy query"));
         if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) wbpc = std::min(wbpc, std::max(1, std::atoi(e)));
         s->grid_wf[mode] = std::max(1, wbpc) * s->cus;
@@ -474,7 +474,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.stats = (unsigned long long *)s->stats;
 
     // engine: the megakernel (default) or the workgroup wavefront (RTNW_ENGINE=wave,
-    // rt_wavefront.hip; no profile variant: a profile request runs it plain)
+    // rt_wavefront.hip)
     const char *eng = std::getenv("RTNW_ENGINE");
     const bool wave = eng && std::strcmp(eng, "wave") == 0;
     if (wave) {
@@ -499,7 +499,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
 
     const float k = (float)(1.0 / (double)(float)p->spp);   // vec3::operator/= (vec3.h:134-141)
     HIP_TRY(hipEventRecord(s->ev[0], stream));
-    if (wave) HIP_TRY(rt_launch_wavefront(&a, s->grid_wf[mode], mode == 2 ? 0 : mode, stream));
+    if (wave) HIP_TRY(rt_launch_wavefront(&a, s->grid_wf[mode], mode, stream));
     else HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
     HIP_TRY(hipEventRecord(s->ev[1], stream));
     HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, nchunks, k, (const uint32_t *)s->job_out, out_dev, stream));

@@ -196,3 +196,25 @@ def test_medium_size_final_parity():
 def test_ppm_from_gpu_mean_matches_oracle_quantiser():
     g = gpu_render("cornell_box", 40, 40, 8, seed=2)
     assert rtnw.ppm_text(rtnw.quantize(g)) == O.ppm_text(O.quantize(g))
+
+
+@pytest.mark.parametrize("scene,nx,ny,ns", [("final", 48, 48, 16), ("cornell_smoke", 32, 32, 8),
+                                            ("random_motion", 40, 20, 8), ("earth", 32, 32, 8)])
+def test_engines_and_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
+    """The megakernel and the workgroup-wavefront engine (RTNW_ENGINE=wave) run the same
+    per-sample arithmetic and sum each work item in sample order, and the closest hit is
+    fixed by (t, list order) whatever the BVH's width: all four combinations must agree
+    bit for bit."""
+    cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene]
+    cam = rtnw.Camera.preset(cam_name, nx, ny)
+    p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, chunk=4, seed=11)
+    out = {}
+    for width in ("2", "4"):
+        monkeypatch.setenv("RTNW_BVH_WIDTH", width)
+        sc = rtnw.Scene.builtin(scene, earth_png=O.EARTH_PNG)   # the width is fixed when the scene is built
+        for engine in ("mega", "wave"):
+            monkeypatch.setenv("RTNW_ENGINE", engine)
+            out[(width, engine)] = sc.render_tile(cam, p, 0, 0, nx, ny)
+    ref = out[("2", "mega")]
+    for key, img in out.items():
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), key

@@ -55,7 +55,12 @@ for step in "$@"; do
             run pmc_d7 600 rocprofv3 --pmc TCP_PENDING_STALL_CYCLES -d gpurun_out/pmc_d7 -o run --output-format csv -- $B
             run pmc_d8 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_FLAT SQ_WAIT_ANY SQ_WAIT_INST_ANY -d gpurun_out/pmc_d8 -o run --output-format csv -- $B
             run pmc_d9 600 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU -d gpurun_out/pmc_d9 -o run --output-format csv -- $B
+            run pmc_d10 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/pmc_d10 -o run --output-format csv -- $B
             python3 tools/pmc_deep.py gpurun_out > gpurun_out/pmc_deep.txt ;;
+    pmc_lanes) export TMPDIR=/tmp
+            B="python3 bench.py --spp ${PMC_SPP:-128} --steps 1 --warmup 0 --no-cpu-baseline"
+            run pmc_l1 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/pmc_l1 -o run --output-format csv -- $B
+            RTNW_ENGINE=wave run pmc_l2w 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/pmc_l2w -o run --output-format csv -- $B ;;
     ab)     run ab 1200 python3 tools/ab.py $AB_LIBS --rounds ${AB_ROUNDS:-2} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -36,5 +36,7 @@ if g:
             print(f"{k:36s} per CU-cycle {vals[k] / cyc / 256:.4f}")
 if "SQC_ICACHE_REQ" in vals:
     print("icache miss rate", vals.get("SQC_ICACHE_MISSES", 0) / max(1, vals["SQC_ICACHE_REQ"]))
+if "SQ_THREAD_CYCLES_VALU" in vals and "SQ_ACTIVE_INST_VALU" in vals:
+    print("VALU lane utilization", vals["SQ_THREAD_CYCLES_VALU"] / (64 * vals["SQ_ACTIVE_INST_VALU"]))
 if "TCP_TOTAL_CACHE_ACCESSES" in vals:
     print("L1 miss rate", vals.get("TCP_CACHE_MISS", 0) / max(1, vals["TCP_TOTAL_CACHE_ACCESSES"]))

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""tools/stage_profile.py — where the megakernel's wave-cycles go (RT_FLAG_PROFILE
-build: s_memtime stamps at the stage boundaries of each loop iteration, summed
-over waves).  Diagnostic only: shares, never timings."""
+"""tools/stage_profile.py — where the engine's wave-cycles go (RT_FLAG_PROFILE
+build: s_memtime stamps at the stage boundaries, summed over waves).  Megakernel:
+claim / traverse / media / shade; wavefront engine (RTNW_ENGINE=wave): phase C /
+phase T / phase S / list building + barrier waits.  Diagnostic only: shares,
+never timings."""
 import json
 import os
 import sys
@@ -32,11 +34,11 @@ print(json.dumps({"scene": scene_name, "image": [nx, ny], "spp": spp, "plain_ker
                   "rays_per_sample": c["segments"] / c["samples"], "grid": out["plain"]["grid"],
                   "simd_efficiency": {
                       "iterations_per_lane_segment": c["wave_iterations"] * 64 / c["segments"],
-                      "node_steps": c["node_visits"] / (64 * c["wave_node_trips"]),
+                      "node_steps": c["node_visits"] / (64 * max(1, c["wave_node_trips"])),
                       "prim_steps": (c["sphere_tests"] + c["rect_tests"] + c["moving_sphere_tests"]
                                      - c["medium_tests"]) / (64 * max(1, c["wave_prim_trips"])),
                       "sphere_draw_rounds": c["lane_sphere_draw_trips"] / (64 * max(1, c["wave_sphere_draw_trips"])),
-                      "wave_node_steps_per_iteration": c["wave_node_trips"] / c["wave_iterations"],
-                      "wave_prim_steps_per_iteration": c["wave_prim_trips"] / c["wave_iterations"],
-                      "wave_sphere_draw_rounds_per_iteration": c["wave_sphere_draw_trips"] / c["wave_iterations"]}},
+                      "wave_node_steps_per_iteration": c["wave_node_trips"] / max(1, c["wave_iterations"]),
+                      "wave_prim_steps_per_iteration": c["wave_prim_trips"] / max(1, c["wave_iterations"]),
+                      "wave_sphere_draw_rounds_per_iteration": c["wave_sphere_draw_trips"] / max(1, c["wave_iterations"])}},
                  indent=1))
