@@ -4,10 +4,12 @@
 * the host API's scene builders + flattener reproduce the reference's scenes
   exactly (leaf dump == reference dump, golden SHA-256);
 * the camera, quantiser and PPM writer match the reference arithmetic;
-* without a GPU, rendering fails loudly (there is no CPU fallback).
+* without a GPU, rendering fails loudly (there is no CPU fallback);
+* the device log of constant_medium (host-compiled from the same header) matches glibc.
 """
 import ctypes
 import hashlib
+import os
 import subprocess
 
 import numpy as np
@@ -15,6 +17,7 @@ import pytest
 
 import oracle as O
 import rtnw
+from conftest import ROOT
 
 
 def test_library_exports_every_header_symbol():
@@ -135,3 +138,23 @@ def test_descriptor_validation_rejects_bad_material():
         assert b"material" in rtnw.lib().rt_last_error()
     finally:
         c.prims[0].material = saved
+
+
+def test_device_log_matches_glibc(tmp_path):
+    """log_f64 (rt_device.h), the device log of constant_medium's free flight
+    (constant_medium.h:36), against glibc's log on counter-stream draws: within 1 ulp,
+    and never a different float hit_distance for a range of densities."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    pkg = os.path.dirname(rtnw.LIB_PATH)
+    exe = str(tmp_path / "log_check")
+    subprocess.run([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(pkg, "csrc"), "-I", os.path.join(pkg, "csrc", "hip"),
+                    os.path.join(ROOT, "tests", "native", "log_check.cpp"), "-o", exe],
+                   check=True, capture_output=True)
+    tested, maxulp, fdiff = (int(v) for v in subprocess.run([exe, "2000000"], check=True, capture_output=True,
+                                                            text=True).stdout.split())
+    assert tested > 2000000
+    assert maxulp <= 1
+    assert fdiff == 0
