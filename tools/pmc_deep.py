@@ -6,7 +6,7 @@ import glob
 import os
 import sys
 
-KERNEL = os.environ.get("RT_PMC_KERNEL", "rt_megakernel<false, false>")
+KERNEL = os.environ.get("RT_PMC_KERNEL", "rt_megakernel<false, false")
 vals = {}
 for path in sorted(glob.glob(os.path.join(sys.argv[1], "pmc_d*", "run_counter_collection.csv"))):
     seen = None

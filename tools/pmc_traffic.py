@@ -17,7 +17,7 @@ import json
 import os
 import sys
 
-KERNEL = os.environ.get("RT_PMC_KERNEL", "rt_megakernel<false, false>")
+KERNEL = os.environ.get("RT_PMC_KERNEL", "rt_megakernel<false, false")
 
 
 def load(path):
