@@ -46,6 +46,11 @@ namespace {
 #define RT_LDS_NODE_F4 508
 #endif
 
+// 1: lanes that reach a leaf keep descending until every lane holds one
+#ifndef RT_SPECULATIVE
+#define RT_SPECULATIVE 1
+#endif
+
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -214,6 +219,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                     --sp;
                     node = stk[sp * 64];
                   }
+                  if (!RT_SPECULATIVE && pleaf != RT_EMPTY_CHILD) break;
                   if (__ballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD) == 0ull) break;
                 }
                 if (pleaf != RT_EMPTY_CHILD) {

@@ -158,3 +158,19 @@ def test_device_log_matches_glibc(tmp_path):
     assert tested > 2000000
     assert maxulp <= 1
     assert fdiff == 0
+
+
+def test_bvh_builder_invariants(tmp_path):
+    """tests/native/bvh_check.cpp: for BVH widths 2 and 4, on every built-in scene and on
+    adversarial synthetic ones (200k uniform, 50k identical, 20k geometric spheres):
+    each primitive in exactly one leaf, child boxes contain their primitives,
+    breadth-first numbering, and the stack bound within the 24-entry LDS stack."""
+    pkg = os.path.dirname(rtnw.LIB_PATH)
+    exe = str(tmp_path / "bvh_check")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(pkg, "csrc"),
+                    "-I", os.path.join(pkg, "csrc", "host"), os.path.join(ROOT, "tests", "native", "bvh_check.cpp"),
+                    "-o", exe, "-L", pkg, "-lrt_hip", f"-Wl,-rpath,{pkg}"], check=True, capture_output=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.strip().endswith("OK")
