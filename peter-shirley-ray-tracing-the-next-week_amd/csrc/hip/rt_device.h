@@ -67,22 +67,24 @@ struct Rng {
 // tools/gen_log_table.py.  Near 1 (x > 0.9375): log1p(x - 1), x - 1 exact.
 // About 30 double operations instead of ocml's ~100.
 __host__ __device__ __forceinline__ double log_f64(double x) {
-    const double d = x - 1.0;   // exact for x in [0.5, 2]
-    double q = 1.0 / 14;
-    q = __builtin_fma(q, d, -1.0 / 13);
-    q = __builtin_fma(q, d, 1.0 / 12);
-    q = __builtin_fma(q, d, -1.0 / 11);
-    q = __builtin_fma(q, d, 1.0 / 10);
-    q = __builtin_fma(q, d, -1.0 / 9);
-    q = __builtin_fma(q, d, 1.0 / 8);
-    q = __builtin_fma(q, d, -1.0 / 7);
-    q = __builtin_fma(q, d, 1.0 / 6);
-    q = __builtin_fma(q, d, -1.0 / 5);
-    q = __builtin_fma(q, d, 1.0 / 4);
-    q = __builtin_fma(q, d, -1.0 / 3);
-    q = __builtin_fma(q, d, 1.0 / 2);
-    const double near1 = __builtin_fma(-(d * d), q, d);   // d - d^2 (1/2 - d/3 + ...)
-
+    if (x > 0.9375) {   // near 1: log1p(d), d = x - 1 exact for x in [0.5, 2]
+        const double d = x - 1.0;
+        double q = 1.0 / 14;
+        q = __builtin_fma(q, d, -1.0 / 13);
+        q = __builtin_fma(q, d, 1.0 / 12);
+        q = __builtin_fma(q, d, -1.0 / 11);
+        q = __builtin_fma(q, d, 1.0 / 10);
+        q = __builtin_fma(q, d, -1.0 / 9);
+        q = __builtin_fma(q, d, 1.0 / 8);
+        q = __builtin_fma(q, d, -1.0 / 7);
+        q = __builtin_fma(q, d, 1.0 / 6);
+        q = __builtin_fma(q, d, -1.0 / 5);
+        q = __builtin_fma(q, d, 1.0 / 4);
+        q = __builtin_fma(q, d, -1.0 / 3);
+        q = __builtin_fma(q, d, 1.0 / 2);
+        return __builtin_fma(-(d * d), q, d);   // d - d^2 (1/2 - d/3 + ...)
+    }
+    if (!(x > 0.0)) return -__builtin_huge_val();
     uint64_t ix;
     __builtin_memcpy(&ix, &x, 8);
     const uint64_t tmp = ix - RT_LOG_OFF;
@@ -100,8 +102,7 @@ __host__ __device__ __forceinline__ double log_f64(double x) {
     const double lo = (w - hi) + r + __builtin_fma(kd, ln2_lo, T[2]);
     const double r2 = r * r;
     const double p = r2 * (-0.5 + r * (1.0 / 3 + r * (-0.25 + r * (0.2 + r * (-1.0 / 6 + r * (1.0 / 7))))));
-    const double far = (lo + p) + hi;
-    return x > 0.9375 ? near1 : (x > 0.0 ? far : -__builtin_huge_val());
+    return (lo + p) + hi;
 }
 
 // pow(x, 5.0) for the x = (double)(float) of schlick (material.h:19).  x has 24
@@ -640,19 +641,49 @@ __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec
 // (best = the surface hit, if any), and the free-flight distance from the
 // medium stream.  Returns the material of the medium that scatters (best_t and
 // `have` updated) or -1.
+// A medium's record and its first boundary primitive's 32-B head, preloaded into
+// LDS once per workgroup (load_media): every lane reads the same address, so the
+// media loop costs no dependent global round trips.
+struct MediumRec {
+    int4 md;      // first boundary prim, count, density bits, material
+    float4 g0;    // first boundary prim: geometry
+    float4 mm;    // first boundary prim: kind | flags, -, instance, order
+};
+#ifndef RT_LDS_MEDIA
+#define RT_LDS_MEDIA 8
+#endif
+__device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds) {
+    const int n = min(A.nmedia, RT_LDS_MEDIA);
+    for (int i = threadIdx.x; i < n; i += RT_BLOCK) {
+        MediumRec m;
+        m.md = A.media[i];
+        m.g0 = A.bprims[m.md.x * 4 + 0];
+        m.mm = A.bprims[m.md.x * 4 + 1];
+        lds[i] = m;
+    }
+}
+
 template <bool kCount>
-__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const Ray &r, int depth, const Rng &g, bool &have,
-                                         float &best_t, Counters &cnt) {
+__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, int depth,
+                                         const Rng &g, bool &have, float &best_t, Counters &cnt) {
     int med_mat = -1;
     for (int k = 0; k < A.nmedia; ++k) {
         if (kCount) cnt.media++;
-        const int4 md = A.media[k];
+        MediumRec M;
+        if (k < RT_LDS_MEDIA) {
+            M = lds_media[k];
+        } else {
+            M.md = A.media[k];
+            M.g0 = A.bprims[M.md.x * 4 + 0];
+            M.mm = A.bprims[M.md.x * 4 + 1];
+        }
+        const int4 md = M.md;
         float r1, r2;
-        const float4 bm = A.bprims[md.x * 4 + 1];
+        const float4 bm = M.mm;
         if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {
             // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
             if (kCount) cnt.spheres++;
-            const float4 sg = A.bprims[md.x * 4 + 0];
+            const float4 sg = M.g0;
             V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
             float a = dot(r.d, r.d);
             float b = dot(oc, r.d);

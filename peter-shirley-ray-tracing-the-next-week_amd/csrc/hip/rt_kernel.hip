@@ -40,12 +40,6 @@ namespace {
 #define RT_READY_BATCH 48
 #endif
 
-// float4 of BVH nodes kept in LDS per workgroup: 508 x 16 B fills the LDS left by
-// 4 workgroups per CU (stacks 24 KB + sampler slots 4 KB each): 127 BVH2 or 72 BVH4 nodes.
-#ifndef RT_LDS_NODE_F4
-#define RT_LDS_NODE_F4 508
-#endif
-
 // 1: lanes that reach a leaf keep descending until every lane holds one
 #ifndef RT_SPECULATIVE
 #define RT_SPECULATIVE 1
@@ -63,17 +57,14 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 template <bool kCount, bool kProf, int kWidth>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;   // float4 per node in HBM
-    constexpr uint32_t kLdsStride = kWidth == 4 ? 7 : 4;    // float4 per node in LDS (BVH4 pad dropped)
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
-    __shared__ float4 lds_nodes[RT_LDS_NODE_F4];
+    __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     const uint32_t lane = lane_id();
     uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
-    // the top of the BVH (a breadth-first prefix) is read from LDS
-    const uint32_t lds_n = min(A.nnodes, (uint32_t)RT_LDS_NODE_F4 / kLdsStride);
-    for (uint32_t i = threadIdx.x; i < lds_n * kLdsStride; i += RT_BLOCK)
-        lds_nodes[i] = A.nodes[(i / kLdsStride) * kNodeStride + i % kLdsStride];
+    // the media records are read from LDS (one broadcast read per medium)
+    load_media(A, lds_media);
     __syncthreads();
 
     // wave-uniform claim pool
@@ -207,10 +198,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                 for (;;) {
                   if (!(node & RT_LEAF_BIT)) {
                     if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
-                    // flat loads: LDS for the top levels, global memory below
-                    const float4 *N = node < lds_n ? (const float4 *)&lds_nodes[node * kLdsStride]
-                                                   : A.nodes + node * kNodeStride;
-                    node = node_step<kWidth>(N, sl, best_t, stk, sp);
+                    node = node_step<kWidth>(A.nodes + node * kNodeStride, sl, best_t, stk, sp);
                   } else if (node != RT_EMPTY_CHILD && pleaf == RT_EMPTY_CHILD) {
                     pleaf = node;   // postpone this leaf, look for the next one
                     node = RT_EMPTY_CHILD;
@@ -260,7 +248,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            const int med_mat = media_hit<kCount>(A, r, depth, g, have, best_t, cnt);
+            const int med_mat = media_hit<kCount>(A, lds_media, r, depth, g, have, best_t, cnt);
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);

@@ -72,6 +72,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
     constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
+    __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ uint16_t lds_list[RT_BLOCK / 64][kWaveSlots];
     __shared__ uint8_t lds_status[RT_BLOCK / 64][kWaveSlots];
 
@@ -96,6 +97,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
 
+    load_media(A, lds_media);
+    __syncthreads();
     for (int k = 0; k < kWaveSlots / 64; ++k) {
         const uint32_t slot = k * 64 + lane;
         status[slot] = ST_CAMERA;
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
             hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
             if (ready) {
                 have = best_prim != kNone;
-                const int med_mat = media_hit<kCount>(A, r, depth, g, have, best_t, cnt);
+                const int med_mat = media_hit<kCount>(A, lds_media, r, depth, g, have, best_t, cnt);
                 if (med_mat >= 0) {
                     hr.p = at(r, best_t);
                     hr.n = mk(1, 0, 0);
