@@ -439,12 +439,14 @@ __device__ __forceinline__ Slab make_slab(const Ray &r, float tmin) {
     s.tmin = tmin;
     return s;
 }
-// entry distance of one child box, +inf if the ray misses it (or the slot is empty)
+// entry distance of one child box, +inf if the ray misses it (or, kSlots, the slot
+// is empty: BVH4 nodes may have unused slots; BVH2 interior nodes never do)
+template <bool kSlots>
 __device__ __forceinline__ float box_entry(const Slab &s, F2 x, F2 y, F2 z, float best_t, uint32_t c) {
     const F2 a = pk_fma(x, s.ix, s.nox), b = pk_fma(y, s.iy, s.noy), e = pk_fma(z, s.iz, s.noz);
     const float tn = vmax3(vmin(a.x, a.y), vmin(b.x, b.y), vmax(vmin(e.x, e.y), s.tmin));
     const float tf = vmin3(vmax(a.x, a.y), vmax(b.x, b.y), vmin(vmax(e.x, e.y), best_t));
-    return (tn <= tf && c != RT_EMPTY_CHILD) ? tn : RT_INF;
+    return (tn <= tf && (!kSlots || c != RT_EMPTY_CHILD)) ? tn : RT_INF;
 }
 __device__ __forceinline__ void cas(float &ka, uint32_t &ca, float &kb, uint32_t &cb) {
     const bool sw = kb < ka;
@@ -463,8 +465,8 @@ __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, fl
     if (kWidth == 2) {   // rt_dnode2
         const float4 b0 = N[0], b1 = N[1], b2 = N[2], cf = N[3];
         const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-        const float k0 = box_entry(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, c0);
-        const float k1 = box_entry(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, c1);
+        const float k0 = box_entry<false>(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, c0);
+        const float k1 = box_entry<false>(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, c1);
         const bool second = k1 < k0;   // ties: child 0 first
         const uint32_t nearc = second ? c1 : c0, farc = second ? c0 : c1;
         const float kn = second ? k1 : k0, kf = second ? k0 : k1;
@@ -475,10 +477,10 @@ __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, fl
         const float4 qx01 = N[0], qx23 = N[1], qy01 = N[2], qy23 = N[3], qz01 = N[4], qz23 = N[5], cf = N[6];
         uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y), c2 = (uint32_t)fbits(cf.z),
                  c3 = (uint32_t)fbits(cf.w);
-        float k0 = box_entry(s, F2{qx01.x, qx01.y}, F2{qy01.x, qy01.y}, F2{qz01.x, qz01.y}, best_t, c0);
-        float k1 = box_entry(s, F2{qx01.z, qx01.w}, F2{qy01.z, qy01.w}, F2{qz01.z, qz01.w}, best_t, c1);
-        float k2 = box_entry(s, F2{qx23.x, qx23.y}, F2{qy23.x, qy23.y}, F2{qz23.x, qz23.y}, best_t, c2);
-        float k3 = box_entry(s, F2{qx23.z, qx23.w}, F2{qy23.z, qy23.w}, F2{qz23.z, qz23.w}, best_t, c3);
+        float k0 = box_entry<true>(s, F2{qx01.x, qx01.y}, F2{qy01.x, qy01.y}, F2{qz01.x, qz01.y}, best_t, c0);
+        float k1 = box_entry<true>(s, F2{qx01.z, qx01.w}, F2{qy01.z, qy01.w}, F2{qz01.z, qz01.w}, best_t, c1);
+        float k2 = box_entry<true>(s, F2{qx23.x, qx23.y}, F2{qy23.x, qy23.y}, F2{qz23.x, qz23.y}, best_t, c2);
+        float k3 = box_entry<true>(s, F2{qx23.z, qx23.w}, F2{qy23.z, qy23.w}, F2{qz23.z, qz23.w}, best_t, c3);
         cas(k0, c0, k1, c1);   // sorting network, nearest first
         cas(k2, c2, k3, c3);
         cas(k0, c0, k2, c2);

@@ -350,17 +350,14 @@ BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, f
     auto emit = [&](auto &out_nodes, auto node_tag) {
         using Node = decltype(node_tag);
         Collapser<Node> c{b, width, {}};
-        if (root2 & RT_LEAF_BIT) {   // tiny scene: wrap the single leaf in a root node
-            Node r{};
-            put_box(r, 0, b.range_box(0, n));
-            r.ch[0] = root2;
-            r.ch[1] = r.ch[2] = r.ch[3] = RT_EMPTY_CHILD;
-            c.out.push_back(r);
-            res.depth = 1;
-        } else {
-            c.collapse(root2, RT_STACK_DEPTH - 1);
-            res.depth = b.max_depth_seen;
+        if (root2 & RT_LEAF_BIT) {   // tiny scene: the single leaf is the root (no nodes)
+            res.depth = 0;
+            res.root = root2;
+            out_nodes = std::move(c.out);
+            return;
         }
+        c.collapse(root2, RT_STACK_DEPTH - 1);
+        res.depth = b.max_depth_seen;
         res.root = 0;
         out_nodes = std::move(c.out);
     };

@@ -112,9 +112,15 @@ int check(const char *name, const rt_prim *prims, int n, const rt_instance *inst
         setenv("RTNW_BVH_WIDTH", width == 4 ? "4" : "2", 1);
         const rtnw::BvhResult r = rtnw::build_bvh(prims, n, inst, t0, t1);
         Checker c{prims, n, r, std::vector<int>(n, 0), ""};
-        // the parent-box check is skipped for children of a node (boxes are the children's own)
-        c.node(width, r.root, nullptr, nullptr);
-        const int bound = c.bound_of(width, r.root);
+        int bound = 0;
+        if (r.root & RT_LEAF_BIT) {   // a single-leaf scene: the leaf is the root
+            const float lo[3] = {-INFINITY, -INFINITY, -INFINITY}, hi[3] = {INFINITY, INFINITY, INFINITY};
+            c.child(width, r.root, lo, hi, 0);
+            if (!(width == 2 ? r.nodes2.empty() : r.nodes4.empty())) c.err = "nodes emitted for a single-leaf scene";
+        } else {
+            c.node(width, r.root, nullptr, nullptr);
+            bound = c.bound_of(width, r.root);
+        }
         for (int i = 0; i < n && c.err.empty(); i++)
             if (c.seen[i] != 1) c.err = "primitive referenced " + std::to_string(c.seen[i]) + " times";
         if (bound > RT_STACK_DEPTH - 1) c.err = "stack bound " + std::to_string(bound) + " exceeds the LDS stack";
