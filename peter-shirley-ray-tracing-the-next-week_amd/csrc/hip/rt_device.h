@@ -44,8 +44,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 __device__ __forceinline__ double u48(uint64_t z) { return (double)(z >> 16) * 0x1p-48; }
-__device__ __forceinline__ uint64_t sample_key(uint64_t seed, uint32_t pixel, uint32_t sample) {
-    return mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) ^ (((uint64_t)pixel << 32) | sample));
+// key of sample (pixel, sample): mix64(seed_key ^ (pixel << 32 | sample)) with
+// seed_key = mix64(seed ^ 0x5851F42D4C957F2D), computed once per launch
+__device__ __forceinline__ uint64_t seed_key(uint64_t seed) { return mix64(seed ^ 0x5851F42D4C957F2Dull); }
+__device__ __forceinline__ uint64_t sample_key(uint64_t skey, uint32_t pixel, uint32_t sample) {
+    return mix64(skey ^ (((uint64_t)pixel << 32) | sample));
 }
 struct Rng {
     uint64_t ctr;    // key + n*GAMMA for the last draw n (n = 0 after start)
@@ -541,6 +544,23 @@ struct CoopSlot {
     uint64_t pad;
 };
 
+// Per requester count m (1..64): the lanes congruent to 0 mod m, and ceil(2^16 / m)
+// (lane / m == (lane * inv) >> 16 exactly for lane < 64).  A wave-uniform index, so
+// a scalar load replaces a scalar loop and an integer division per round.
+struct CoopTable {
+    uint64_t stride_mask[65];
+    uint32_t inv[65];
+    constexpr CoopTable() : stride_mask(), inv() {
+        for (int m = 1; m <= 64; ++m) {
+            uint64_t p = 0;
+            for (int b = 0; b < 64; b += m) p |= 1ull << b;
+            stride_mask[m] = p;
+            inv[m] = (0xFFFFu + (uint32_t)m) / (uint32_t)m;
+        }
+    }
+};
+__constant__ const CoopTable kCoop = CoopTable();
+
 template <int K, bool kCount, class Cand>
 __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt, Cand cand) {
     V3 res = mk(0, 0, 0);
@@ -548,16 +568,13 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
     uint64_t U = __ballot(pending);
     while (U != 0ull) {
         const uint32_t m = (uint32_t)__popcll(U);            // wave-uniform
-        uint64_t P = 0;                                        // lanes congruent to 0 mod m
-        for (uint32_t b = 0; b < 64; b += m) P |= 1ull << b;
+        const uint64_t P = kCoop.stride_mask[m];               // lanes congruent to 0 mod m
         const uint32_t r = lanes_below(U);
         if (pending) slots[r].ctr = g.ctr;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // t = lane / m exactly: lane < 64, m <= 64, inv = ceil(2^16 / m)
-        const uint32_t inv = (0xFFFFu + m) / m;
-        const uint32_t t = (lane * inv) >> 16;
+        const uint32_t t = (lane * kCoop.inv[m]) >> 16;       // lane / m
         const uint32_t slot = lane - t * m;
         const uint64_t base = slots[slot].ctr + (uint64_t)(K * t) * kGamma;
         V3 p;

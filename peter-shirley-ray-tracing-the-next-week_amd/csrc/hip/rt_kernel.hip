@@ -67,6 +67,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
     load_media(A, lds_media);
     __syncthreads();
 
+    const uint64_t skey = seed_key(A.seed);   // per-launch part of the sample keys
     // wave-uniform claim pool
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         float cu_ = 0, cv_ = 0;
         if (starting) {
             int j = A.ny - 1 - (int)py;
-            g.start(sample_key(A.seed, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
+            g.start(sample_key(skey, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
             cu_ = (float)((double)(int)px + g.next()) / (float)A.nx;
             cv_ = (float)((double)j + g.next()) / (float)A.ny;
         }

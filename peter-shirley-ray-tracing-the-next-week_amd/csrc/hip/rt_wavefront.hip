@@ -93,6 +93,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
         }
     };
 
+    const uint64_t skey = seed_key(A.seed);   // per-launch part of the sample keys
     // wave-uniform work-item pool (one global atomic per 64 items)
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 const uint32_t xy = A.job_xy[sm.x - (sm.x / A.npix) * A.npix];
                 px = xy & 0xFFFFu;
                 j = A.ny - 1 - (int)(xy >> 16);
-                g.start(sample_key(A.seed, (uint32_t)(j * A.nx + (int)px), sm.y + A.sample_offset));
+                g.start(sample_key(skey, (uint32_t)(j * A.nx + (int)px), sm.y + A.sample_offset));
                 cu_ = (float)((double)(int)px + g.next()) / (float)A.nx;
                 cv_ = (float)((double)j + g.next()) / (float)A.ny;
             }
