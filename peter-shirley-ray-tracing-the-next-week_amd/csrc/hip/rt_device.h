@@ -126,33 +126,17 @@ __device__ __forceinline__ double pow5(double x) {
 __device__ __forceinline__ float4 ld4(const float4 *p, uint32_t i) { return p[i]; }
 __device__ __forceinline__ int fbits(float f) { return __float_as_int(f); }
 
-// BVH slab test primitives.  Packed FP32 FMA for the lo/hi plane pairs; min/max
-// as plain VALU ops: their operands are never signalling NaNs (FMA results, t_min,
-// the current best t), so the IEEE-mode quieting the compiler would add per use
-// of a loop-carried value is dead weight.  (minnum semantics: a NaN plane distance
-// from an axis-parallel ray leaves that axis unconstrained, i.e. conservative.)
+// BVH slab test primitives: packed FP32 FMA for the lo/hi plane pairs, IEEE
+// min/max (minnum: a NaN plane distance from an axis-parallel ray leaves that axis
+// unconstrained, i.e. conservative).  Plain builtins, not inline asm: the
+// compiler forms v_min3/v_max3 itself, and inline asm would make its hazard
+// recognizer pad the sequence with s_nop (an issue slot each).
 typedef float F2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ F2 pk_fma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ float vmin(float a, float b) {
-    float r;
-    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ float vmax(float a, float b) {
-    float r;
-    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ float vmin3(float a, float b, float c) {
-    float r;
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
+__device__ __forceinline__ float vmin(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ float vmin3(float a, float b, float c) { return vmin(vmin(a, b), c); }
+__device__ __forceinline__ float vmax3(float a, float b, float c) { return vmax(vmax(a, b), c); }
 
 // Ray into the object space of an instance chain (hitable.h:66-67, 129-135).
 __device__ __forceinline__ Ray to_object(const float4 *insts, int inst, Ray r) {
@@ -439,7 +423,7 @@ __device__ __forceinline__ Slab make_slab(const Ray &r, float tmin) {
     Slab s;
     s.ix = F2{ix, ix}; s.iy = F2{iy, iy}; s.iz = F2{iz, iz};
     s.nox = F2{-r.o.x * ix, -r.o.x * ix}; s.noy = F2{-r.o.y * iy, -r.o.y * iy}; s.noz = F2{-r.o.z * iz, -r.o.z * iz};
-    s.tmin = tmin;
+    s.tmin = __builtin_canonicalizef(tmin);   // known canonical: no re-quieting per use
     return s;
 }
 // entry distance of one child box, +inf if the ray misses it (or, kSlots, the slot
