@@ -226,27 +226,47 @@ __device__ __forceinline__ float rect_t(int kind, float4 g0, float k, const Ray 
 // prim kinds: 0 sphere, 1 moving sphere, 2 xy, 3 xz, 4 yz  (rect axis = 2, 1, 0)
 __device__ __forceinline__ int rect_axis(int kind) { return 4 - kind; }
 
-// Test of one primitive whose 32-B head (g0, mm) is already loaded.
+// Test of one primitive whose 32-B head (g0, mm) is already loaded.  Written
+// for a wave whose lanes test different kinds: the sphere terms and the rect's
+// plane terms are computed with selects rather than per-kind branches, and the
+// first quotient — (-b - sqrt(disc)) / a for a sphere (sphere.h:33), (k - o_a) / d_a
+// for a rect (aarect.h:51) — is ONE IEEE division either way.  Every value is the
+// same float the per-kind code computes (same operands, same operations); only
+// the moving-sphere centre and a sphere's second root stay behind branches.
 __device__ __forceinline__ float prim_t_head(float4 g0, float4 mm, const float4 *P, const float4 *insts, uint32_t idx,
                                              const Ray &r0, float tmin, int &key, int &kind_out) {
-    int kind = fbits(mm.x) & 0xff;
-    int inst = fbits(mm.z);
-    int order = fbits(mm.w);
+    const int kind = fbits(mm.x) & 0xff;
+    const int inst = fbits(mm.z);
+    const int order = fbits(mm.w);
     kind_out = kind | (inst >= 0 ? 0x100 : 0);
     Ray r = r0;
     if (inst >= 0) r = to_object(insts, inst, r0);
-    float t;
-    if (kind == RT_PRIM_SPHERE) {
-        t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, r, tmin);
-        key = order;
-    } else if (kind == RT_PRIM_MOVING_SPHERE) {
-        t = sphere_t(msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time), g0.w, r, tmin);
-        key = order;
-    } else {
-        t = rect_t(kind, g0, mm.y, r, tmin);
-        key = -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
+    const bool sph = kind <= RT_PRIM_MOVING_SPHERE;
+    key = sph ? order : -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
+    // sphere.h:25-52 (moving: the centre at r.time, sphere.h:81-83)
+    V3 c = mk(g0.x, g0.y, g0.z);
+    if (kind == RT_PRIM_MOVING_SPHERE) c = msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time);
+    const V3 oc = sub(r.o, c);
+    const float a = dot(r.d, r.d);
+    const float b = dot(oc, r.d);
+    const float cc = dot(oc, oc) - g0.w * g0.w;
+    const float disc = b * b - a * cc;
+    const float sq = sqrtf(disc);
+    // aarect.h:50-100: ray along the plane normal (oa, da) and the two in-plane axes
+    const bool xy = kind == RT_PRIM_XY_RECT, xz = kind == RT_PRIM_XZ_RECT;
+    const float oa = xy ? r.o.z : (xz ? r.o.y : r.o.x), da = xy ? r.d.z : (xz ? r.d.y : r.d.x);
+    const float oi = xy || xz ? r.o.x : r.o.y, di = xy || xz ? r.d.x : r.d.y;
+    const float oj = xy ? r.o.y : r.o.z, dj = xy ? r.d.y : r.d.z;
+    const float t = (sph ? -b - sq : mm.y - oa) / (sph ? a : da);
+    if (sph) {
+        if (!(disc > 0)) return RT_INF;
+        if (t < RT_FLT_MAX && t > tmin) return t;
+        const float t2 = (-b + sq) / a;
+        return (t2 < RT_FLT_MAX && t2 > tmin) ? t2 : RT_INF;
     }
-    return t;
+    if (t < tmin || t > RT_FLT_MAX) return RT_INF;
+    const float ai = oi + t * di, bj = oj + t * dj;
+    return (ai < g0.x || ai > g0.y || bj < g0.z || bj > g0.w) ? RT_INF : t;
 }
 
 __device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float tmin,
