@@ -702,8 +702,9 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
         }
         const int4 md = M.md;
         float r1, r2;
+        bool ok;
         const float4 bm = M.mm;
-        if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {
+        if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {   // wave-uniform
             // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
             if (kCount) cnt.spheres++;
             const float4 sg = M.g0;
@@ -712,36 +713,40 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
             float b = dot(oc, r.d);
             float cc = dot(oc, oc) - sg.w * sg.w;
             float disc = b * b - a * cc;
-            if (!(disc > 0)) continue;
-            const float ta = (-b - sqrtf(disc)) / a;
-            const float tb = (-b + sqrtf(disc)) / a;
-            if (ta < RT_FLT_MAX && ta > -RT_FLT_MAX) r1 = ta;
-            else if (tb < RT_FLT_MAX && tb > -RT_FLT_MAX) r1 = tb;
-            else continue;
+            const bool valid = disc > 0;
+            if (__ballot(valid) == 0ull) continue;   // the whole wave misses the boundary
+            const float sq = sqrtf(disc);
+            const float ta = (-b - sq) / a;
+            const float tb = (-b + sq) / a;
+            // selects, not branches: sphere.h:33-44 for t_min = -FLT_MAX, then t_min = r1 + 0.0001
+            const bool fa = ta < RT_FLT_MAX && ta > -RT_FLT_MAX, fb = tb < RT_FLT_MAX && tb > -RT_FLT_MAX;
+            r1 = fa ? ta : tb;
             const float tmin2 = (float)((double)r1 + 0.0001);
-            if (ta < RT_FLT_MAX && ta > tmin2) r2 = ta;
-            else if (tb < RT_FLT_MAX && tb > tmin2) r2 = tb;
-            else continue;
+            const bool ga = ta < RT_FLT_MAX && ta > tmin2, gb = tb < RT_FLT_MAX && tb > tmin2;
+            r2 = ga ? ta : tb;
+            ok = valid && (fa || fb) && (ga || gb);
         } else {
             r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
-            if (r1 == RT_INF) continue;
+            ok = r1 != RT_INF;
+            if (__ballot(ok) == 0ull) continue;
             r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
-            if (r2 == RT_INF) continue;
+            ok = ok && r2 != RT_INF;
         }
-        float tmax = have ? best_t : RT_FLT_MAX;
-        if (r1 < A.tmin) r1 = A.tmin;
-        if (r2 > tmax) r2 = tmax;
-        if (r1 >= r2) continue;
-        if (r1 < 0) r1 = 0;
-        float dlen = len(r.d);
-        float distance_inside_boundary = (r2 - r1) * dlen;
-        float density = __int_as_float(md.z);
-        float hit_distance = (float)((double)(-(1 / density)) * log_f64(g.medium(depth, k)));
-        if (hit_distance < distance_inside_boundary) {
-            best_t = r1 + hit_distance / dlen;
-            have = true;
-            med_mat = md.w;
-        }
+        const float tmax = have ? best_t : RT_FLT_MAX;
+        r1 = r1 < A.tmin ? A.tmin : r1;
+        r2 = r2 > tmax ? tmax : r2;
+        ok = ok && !(r1 >= r2);
+        if (__ballot(ok) == 0ull) continue;   // no lane inside the medium: no free-flight draw
+        r1 = r1 < 0 ? 0.f : r1;
+        const float dlen = len(r.d);
+        const float distance_inside_boundary = (r2 - r1) * dlen;
+        const float density = __int_as_float(md.z);
+        const float hit_distance = (float)((double)(-(1 / density)) * log_f64(g.medium(depth, k)));
+        const bool hit = ok && hit_distance < distance_inside_boundary;
+        const float tm = r1 + hit_distance / dlen;
+        best_t = hit ? tm : best_t;
+        have = have || hit;
+        med_mat = hit ? md.w : med_mat;
     }
     return med_mat;
 }
