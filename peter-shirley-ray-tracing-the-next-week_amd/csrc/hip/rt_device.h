@@ -565,6 +565,9 @@ struct CoopTable {
 };
 __constant__ const CoopTable kCoop = CoopTable();
 
+// One candidate per lane and round (two per lane measured slower: the extra
+// candidate costs every lane more than the saved rounds).  Candidate position
+// c = lane belongs to slot c mod m as that owner's candidate c / m.
 template <int K, bool kCount, class Cand>
 __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt, Cand cand) {
     V3 res = mk(0, 0, 0);
@@ -572,36 +575,30 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
     uint64_t U = __ballot(pending);
     while (U != 0ull) {
         const uint32_t m = (uint32_t)__popcll(U);            // wave-uniform
+        const uint32_t inv = kCoop.inv[m];
         const uint64_t P = kCoop.stride_mask[m];               // lanes congruent to 0 mod m
         const uint32_t r = lanes_below(U);
         if (pending) slots[r].ctr = g.ctr;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t t = (lane * kCoop.inv[m]) >> 16;       // lane / m
+        const uint32_t t = (lane * inv) >> 16;                 // lane / m
         const uint32_t slot = lane - t * m;
         const uint64_t base = slots[slot].ctr + (uint64_t)(K * t) * kGamma;
         V3 p;
-        const bool ok = cand(base, p);
-        const uint64_t okm = __ballot(ok);
+        const uint64_t okm = __ballot(cand(base, p));
         if (kCount && first_active()) cnt.w_rius++;
         uint32_t src = lane;
         bool won = false;
         if (pending) {
-            const uint64_t mine = P << r;
-            const uint64_t win = okm & mine;
-            if (win != 0ull) {
-                src = (uint32_t)__builtin_ctzll(win);
-                const uint32_t tried = (uint32_t)__popcll(mine & ((1ull << src) - 1ull)) + 1u;
-                g.ctr += (uint64_t)(K * tried) * kGamma;
-                if (kCount) cnt.l_rius += tried;
-                won = true;
-                pending = false;
-            } else {
-                const uint32_t tried = (uint32_t)__popcll(mine);
-                g.ctr += (uint64_t)(K * tried) * kGamma;
-                if (kCount) cnt.l_rius += tried;
-            }
+            const uint64_t win = okm & (P << r);
+            won = win != 0ull;
+            src = won ? (uint32_t)__builtin_ctzll(win) : lane;
+            // candidates consumed: up to the winner, or all of the owner's this round
+            const uint32_t tried = ((won ? src : 63u - r) * inv >> 16) + 1u;
+            g.ctr += (uint64_t)(K * tried) * kGamma;
+            if (kCount) cnt.l_rius += tried;
+            pending = !won;
         }
         // every lane takes part in the exchange (bpermute reads the source lane's register)
         const float px = __shfl(p.x, (int)src), py = __shfl(p.y, (int)src), pz = __shfl(p.z, (int)src);
