@@ -66,27 +66,12 @@ struct Rng {
 // result only feeds a float rounding of (double)(-1/density) * log(u), which a
 // last-bit difference changes with probability ~2^-29.  Table path (glibc's
 // scheme): x = 2^k z, z in [0.6875, 1.375), log x = k ln2 + log(1/invc) + log1p(r),
-// r = fma(z, invc, -1), |r| < 0.006, log(1/invc) a double-double from
-// tools/gen_log_table.py.  Near 1 (x > 0.9375): log1p(x - 1), x - 1 exact.
-// About 30 double operations instead of ocml's ~100.
+// r = fma(z, invc, -1), |r| < 0.004, log(1/invc) a double-double from
+// tools/gen_log_table.py.  The row for [1 - 2^-8, 1) has invc = 1 and log(1/invc) = 0,
+// so next to 1 the result is r + r^2 p(r) with r = x - 1 exact: relatively accurate
+// without glibc's separate near-1 path (a branch nearly every wave took for some lane).
+// About 25 double operations instead of ocml's ~100.
 __host__ __device__ __forceinline__ double log_f64(double x) {
-    if (x > 0.9375) {   // near 1: log1p(d), d = x - 1 exact for x in [0.5, 2]
-        const double d = x - 1.0;
-        double q = 1.0 / 14;
-        q = __builtin_fma(q, d, -1.0 / 13);
-        q = __builtin_fma(q, d, 1.0 / 12);
-        q = __builtin_fma(q, d, -1.0 / 11);
-        q = __builtin_fma(q, d, 1.0 / 10);
-        q = __builtin_fma(q, d, -1.0 / 9);
-        q = __builtin_fma(q, d, 1.0 / 8);
-        q = __builtin_fma(q, d, -1.0 / 7);
-        q = __builtin_fma(q, d, 1.0 / 6);
-        q = __builtin_fma(q, d, -1.0 / 5);
-        q = __builtin_fma(q, d, 1.0 / 4);
-        q = __builtin_fma(q, d, -1.0 / 3);
-        q = __builtin_fma(q, d, 1.0 / 2);
-        return __builtin_fma(-(d * d), q, d);   // d - d^2 (1/2 - d/3 + ...)
-    }
     if (!(x > 0.0)) return -__builtin_huge_val();
     uint64_t ix;
     __builtin_memcpy(&ix, &x, 8);
@@ -665,7 +650,7 @@ __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec
 // LDS once per workgroup (load_media): every lane reads the same address, so the
 // media loop costs no dependent global round trips.
 struct MediumRec {
-    int4 md;      // first boundary prim, count, density bits, material
+    int4 md;      // first boundary prim, count, -(1/density) bits, material
     float4 g0;    // first boundary prim: geometry
     float4 mm;    // first boundary prim: kind | flags, -, instance, order
 };
@@ -737,8 +722,8 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
         r1 = r1 < 0 ? 0.f : r1;
         const float dlen = len(r.d);
         const float distance_inside_boundary = (r2 - r1) * dlen;
-        const float density = __int_as_float(md.z);
-        const float hit_distance = (float)((double)(-(1 / density)) * log_f64(g.medium(depth, k)));
+        const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
+        const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k)));
         const bool hit = ok && hit_distance < distance_inside_boundary;
         const float tm = r1 + hit_distance / dlen;
         best_t = hit ? tm : best_t;

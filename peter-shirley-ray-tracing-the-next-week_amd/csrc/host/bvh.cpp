@@ -103,9 +103,12 @@ struct Node2 {
 };
 
 struct Builder {
+    static constexpr int kMaxBins = 256;
     // SAH leaves hold at most 2 primitives: on final() that measured ~2% faster than 4 or 8
     // (tools/ab.py); RTNW_BVH_MAX_LEAF overrides (<= RT_MAX_LEAF) for experiments.
     int max_leaf = 2;
+    int bins = 32;           // SAH bins per axis (<= kMaxBins)
+    double trav_cost = 1.0;  // SAH node-step cost relative to one primitive test
     std::vector<Item> items;
     std::vector<Node2> nodes;
     std::vector<int> order;   // leaf order -> original prim index
@@ -147,23 +150,23 @@ struct Builder {
             return mid;
         }
 
-        constexpr int kBins = 32;
+        const int kBins = bins;
         const double parent_area = range_box(begin, end).area();
         double best_cost = 1e300;
         int best_axis = -1, best_bin = -1;
         for (int k = 0; k < 3; k++) {
             const double e = cb.hi[k] - cb.lo[k];
             if (e <= 0) continue;
-            Box bins[kBins];
-            int counts[kBins] = {0};
+            Box bins[kMaxBins];
+            int counts[kMaxBins] = {0};
             for (int i = begin; i < end; i++) {
                 int bi = (int)((items[i].c[k] - cb.lo[k]) / e * kBins);
                 bi = std::min(std::max(bi, 0), kBins - 1);
                 counts[bi]++;
                 bins[bi].grow(items[i].box);
             }
-            double right_area[kBins];
-            int right_count[kBins];
+            double right_area[kMaxBins];
+            int right_count[kMaxBins];
             Box acc;
             int cnt = 0;
             for (int b = kBins - 1; b > 0; b--) {
@@ -178,7 +181,7 @@ struct Builder {
                 lacc.grow(bins[b - 1]);
                 lcnt += counts[b - 1];
                 if (lcnt == 0 || right_count[b] == 0) continue;
-                const double cost = 1.0 + (lacc.area() * lcnt + right_area[b] * right_count[b]) / parent_area;
+                const double cost = trav_cost + (lacc.area() * lcnt + right_area[b] * right_count[b]) / parent_area;
                 if (cost < best_cost) { best_cost = cost; best_axis = k; best_bin = b; }
             }
         }
@@ -335,6 +338,8 @@ BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, f
     if (n <= 0) return res;
     const double ta = std::min(0.0, (double)time0), tb = std::max(0.0, (double)time1);
     Builder b;
+    if (const char *e = std::getenv("RTNW_SAH_BINS")) b.bins = std::max(2, std::min(Builder::kMaxBins, std::atoi(e)));
+    if (const char *e = std::getenv("RTNW_SAH_TRAV")) b.trav_cost = std::atof(e);
     if (const char *e = std::getenv("RTNW_BVH_MAX_LEAF")) b.max_leaf = std::max(1, std::min(RT_MAX_LEAF, std::atoi(e)));
     b.items.resize(n);
     for (int i = 0; i < n; i++) {

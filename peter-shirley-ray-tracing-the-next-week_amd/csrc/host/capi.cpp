@@ -317,7 +317,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     for (int i = 0; i < d->nmedia; i++) {
         media[i].first = d->media[i].boundary_first;
         media[i].count = d->media[i].boundary_count;
-        media[i].density = d->media[i].density;
+        media[i].neg_inv_density = -(1 / d->media[i].density);   // constant_medium.h:36
         media[i].material = d->media[i].material;
     }
     std::vector<float> ranvec(256 * 4, 0.0f);

@@ -89,10 +89,12 @@ struct rt_dinstance {
     float ops[RT_MAX_INSTANCE_OPS][4];
 };
 
-// Medium, 16 B: (boundary_first, boundary_count, density, phase material)
+// Medium, 16 B: (boundary_first, boundary_count, -(1/density), phase material).
+// The float -(1/density) of constant_medium.h:36 is computed once on the host
+// (IEEE division, the same value the device would get per ray).
 struct rt_dmedium {
     int32_t first, count;
-    float density;
+    float neg_inv_density;
     int32_t material;
 };
 
