@@ -85,11 +85,16 @@ __host__ __device__ __forceinline__ double log_f64(double x) {
     const double r = __builtin_fma(z, T[0], -1.0);
     const double kd = (double)k;
     const double ln2_hi = 0x1.62e42fefa3800p-1, ln2_lo = 0x1.ef35793c76730p-45;   // kd * ln2_hi exact
-    const double w = kd * ln2_hi + T[1];
+    const double w = __builtin_fma(kd, ln2_hi, T[1]);   // kd * ln2_hi is exact: same as mul + add
     const double hi = w + r;
     const double lo = (w - hi) + r + __builtin_fma(kd, ln2_lo, T[2]);
     const double r2 = r * r;
-    const double p = r2 * (-0.5 + r * (1.0 / 3 + r * (-0.25 + r * (0.2 + r * (-1.0 / 6 + r * (1.0 / 7))))));
+    double q = __builtin_fma(r, 1.0 / 7, -1.0 / 6);
+    q = __builtin_fma(q, r, 0.2);
+    q = __builtin_fma(q, r, -0.25);
+    q = __builtin_fma(q, r, 1.0 / 3);
+    q = __builtin_fma(q, r, -0.5);
+    const double p = r2 * q;
     return (lo + p) + hi;
 }
 
@@ -818,10 +823,10 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
             outward_normal = neg(hr.n);
             ni_over_nt = ref_idx;
             cosine = dot(r.d, hr.n) / len(r.d);
-            cosine = sqrtf(1 - ref_idx * ref_idx * (1 - cosine * cosine));
+            cosine = sqrtf(1 - m1.z * (1 - cosine * cosine));   // m1.z = ref_idx * ref_idx
         } else {
             outward_normal = hr.n;
-            ni_over_nt = (float)(1.0 / (double)ref_idx);
+            ni_over_nt = m1.x;                                   // (float)(1.0 / (double)ref_idx)
             cosine = -dot(r.d, hr.n) / len(r.d);
         }
         // refract, material.h:23-33
@@ -833,8 +838,7 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
         if (disc > 0) {
             refracted = sub(scale(ni_over_nt, sub(uv, scale(dt, outward_normal))), scale(sqrtf(disc), outward_normal));
             // schlick, material.h:16-20
-            float r0 = (1 - ref_idx) / (1 + ref_idx);
-            r0 = r0 * r0;
+            const float r0 = m1.y;   // ((1 - ref_idx) / (1 + ref_idx))^2, host-side
             reflect_prob = (float)(r0 + (double)(1 - r0) * pow5((double)(1 - cosine)));
         } else {
             reflect_prob = 1.0f;

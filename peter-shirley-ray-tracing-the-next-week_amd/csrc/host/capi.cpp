@@ -285,6 +285,14 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         o.fuzz = m.fuzz;
         o.ref_idx = m.ref_idx;
         for (int k = 0; k < 3; k++) o.albedo[k] = m.albedo[k];
+        if (m.kind == RT_MAT_DIELECTRIC) {
+            // a dielectric has no albedo (material.h:99): its slots carry the per-material
+            // constants of material.h:103-116 in the reference's float/double arithmetic
+            const float r0 = (1 - m.ref_idx) / (1 + m.ref_idx);
+            o.albedo[0] = (float)(1.0 / (double)m.ref_idx);   // ni_over_nt entering
+            o.albedo[1] = r0 * r0;                            // schlick's r0^2
+            o.albedo[2] = m.ref_idx * m.ref_idx;              // ref_idx^2 of the exit cosine
+        }
         o.flags = (m.texture >= 0 && reads_uv(m.texture)) ? 1 : 0;
     }
     std::vector<rt_dtexture> texs(d->ntextures);

@@ -67,7 +67,8 @@ struct rt_dprim {
     float g1[4], g2[4];
 };
 
-// Material, 32 B: (kind, texture, fuzz, ref_idx) + (albedo.xyz, flags)
+// Material, 32 B: (kind, texture, fuzz, ref_idx) + (albedo.xyz, flags).  A dielectric
+// carries (float)(1.0/(double)ref_idx), schlick r0^2 and ref_idx^2 in albedo (capi.cpp).
 struct rt_dmaterial {
     int32_t kind, texture;
     float fuzz, ref_idx;
