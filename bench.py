@@ -104,6 +104,28 @@ def read_traffic(samples_per_launch):
         return None
 
 
+def end_to_end(cam, params, nx, ny, dev):
+    """SURVEY §8d's second reading of the metric: one more render of the same
+    workload timed from scene creation (flatten, SAH build, upload to HBM) through
+    the render to the framebuffer in host memory.  Reported beside `value`, never as
+    it (`value` starts with the scene resident)."""
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    scene = rtnw.Scene.builtin("final", device=dev.index)
+    t1 = time.perf_counter()
+    out = torch.empty(nx * ny * 3, dtype=torch.float32, device=dev)
+    scene.render_tiles(cam, params, [(0, 0, nx, ny)], out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    host = out.cpu()
+    t3 = time.perf_counter()
+    scene.close()
+    del host
+    return {"value": nx * ny * params.spp / (t3 - t0) / 1e6, "unit": "Msamples/s",
+            "includes": "scene create (flatten + SAH BVH + HBM upload) + render + framebuffer readback",
+            "scene_create_ms": (t1 - t0) * 1e3, "render_ms": (t2 - t1) * 1e3, "readback_ms": (t3 - t2) * 1e3}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,6 +246,8 @@ def main():
                          "algorithmic_bytes_per_sample": alg / max(1.0, cst["samples"])},
             "cpu_baseline": None,
         }
+        if world == 1:
+            res["end_to_end"] = end_to_end(cam, params, nx, ny, dev)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(min(16, os.cpu_count() or 1))
         print(json.dumps(res), flush=True)

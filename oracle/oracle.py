@@ -21,6 +21,7 @@ REF_BIN = os.path.join(HERE, "_ref", "ref_render")
 SCENES = {
     "random_scene": 0, "random_motion": 1, "cornell_box": 2, "cornell_smoke": 3,
     "final": 4, "simple_light": 5, "two_spheres": 6, "test": 7, "earth": 8,
+    "edge_empty": 9, "edge_single": 10, "edge_degenerate": 11,   # the tests' edge cases (ref_harness.cpp edge_*)
 }
 EARTH_PNG = os.path.join(os.path.dirname(HERE), "tests", "golden", "picture.png")   # main.cpp:93's asset
 CAMERAS = {"cornell": 0, "random": 1, "final_alt": 2}
@@ -36,6 +37,9 @@ SCENE_DEFAULTS = {
     "two_spheres": dict(camera="random", background="black", max_depth=50),
     "test": dict(camera="random", background="black", max_depth=50),
     "earth": dict(camera="cornell", background="black", max_depth=50),
+    "edge_empty": dict(camera="random", background="sky", max_depth=50),
+    "edge_single": dict(camera="random", background="sky", max_depth=50),
+    "edge_degenerate": dict(camera="random", background="sky", max_depth=50),
 }
 
 

@@ -228,13 +228,44 @@ static void dump_node(const hitable *h, const std::string &wrap) {
     fprintf(g_dump, "%sunknown\n", wrap.c_str());
 }
 
+// ------------------------------------------------------------ edge scenes
+// Edge cases of this build's tests, written with the reference's own classes so
+// the oracle's restatement is pinned on them as on the book's scenes (the same
+// three scenes: oracle/rt_oracle.c build_edge_*, csrc/host/rtnw.cpp edge_*).
+static hitable *edge_empty() { return new hitable_list(new hitable *[1], 0); }
+static hitable *edge_single() {
+    hitable **l = new hitable *[1];
+    l[0] = new sphere(vec3(0, 1, 0), 1, new lambertian(new constant_texture(vec3(0.5, 0.5, 0.5))));
+    return new hitable_list(l, 1);
+}
+static hitable *edge_degenerate() {
+    hitable **l = new hitable *[11];
+    int i = 0;
+    material *glass = new dielectric(1.5);
+    l[i++] = new sphere(vec3(0, -1000, 0), 1000, new lambertian(new constant_texture(vec3(0.5, 0.5, 0.5))));
+    l[i++] = new sphere(vec3(0, 1, 0), 0, new lambertian(new constant_texture(vec3(0.8, 0.3, 0.3))));   // zero radius
+    l[i++] = new sphere(vec3(-2.5, 1, 0), -1, glass);                                                  // negative radius
+    l[i++] = new sphere(vec3(2.5, 1, 0), 1, glass);                                                    // hollow bubble
+    l[i++] = new sphere(vec3(2.5, 1, 0), -0.9, glass);
+    l[i++] = new xz_rect(-1, -1, -1, 1, 0.5, new diffuse_light(new constant_texture(vec3(4, 4, 4))));   // zero width
+    l[i++] = new moving_sphere(vec3(1, 0.5, 1.5), vec3(1, 0.5, 2), 0.5, 0.5, 0.5,                        // zero shutter span
+                               new lambertian(new constant_texture(vec3(0.2, 0.8, 0.2))));
+    l[i++] = new sphere(vec3(-1, 0.7, 1.5), 0.7, new metal(vec3(0.7, 0.6, 0.5), 1.5));                  // fuzz clamped to 1
+    l[i++] = new constant_medium(new sphere(vec3(1, 0.5, -1.5), 0.5, glass), 0, new constant_texture(vec3(1, 1, 1)));
+    l[i++] = new constant_medium(new sphere(vec3(-1, 0.5, -1.5), 0.5, glass), 1e30,
+                                 new constant_texture(vec3(0.9, 0.9, 0.9)));
+    l[i++] = new flip_normals(new xy_rect(-3, 3, 0, 3, -3, new diffuse_light(new constant_texture(vec3(2, 2, 2)))));
+    return new hitable_list(l, i);
+}
+
 // ----------------------------------------------------------------------- CLI
 static void usage() {
     fprintf(stderr,
         "ref_render --scene NAME [--nx N --ny N --ns N --depth D --bg black|sky --tmin T]\n"
         "           [--cam cornell|random|final_alt] [--rng canonical|counter --seed S]\n"
         "           [--rows J0:J1] [--ppm FILE] [--fb FILE] [--dump FILE] [--perlin FILE] [--time]\n"
-        "  scenes: random_scene random_motion cornell_box cornell_smoke final simple_light two_spheres test\n");
+        "  scenes: random_scene random_motion cornell_box cornell_smoke final simple_light two_spheres test\n"
+        "          edge_empty edge_single edge_degenerate (sky, random camera)\n");
     exit(2);
 }
 
@@ -288,6 +319,9 @@ int main(int argc, char **argv) {
     else if (scene == "simple_light") { world = simple_light(); cam_default = "random"; }
     else if (scene == "two_spheres") { world = two_spheres(); cam_default = "random"; }
     else if (scene == "test") { world = test(); cam_default = "random"; }
+    else if (scene == "edge_empty") { world = edge_empty(); sky_default = true; cam_default = "random"; }
+    else if (scene == "edge_single") { world = edge_single(); sky_default = true; cam_default = "random"; }
+    else if (scene == "edge_degenerate") { world = edge_degenerate(); sky_default = true; cam_default = "random"; }
     else if (scene == "earth") {   // stbi_load("picture.png") reads the working directory (main.cpp:93)
         if (!assets.empty() && chdir(assets.c_str()) != 0) { perror("chdir"); return 2; }
         world = earth();

@@ -661,6 +661,31 @@ static obj_t *build_test(scene_t *s) {                                    /* mai
     return o_list(s, list, 3);
 }
 
+/* Edge scenes of the tests, the same objects as oracle/ref_harness.cpp edge_*. */
+static obj_t *build_edge_empty(scene_t *s) { return o_list(s, o_array(s, 1), 0); }
+static obj_t *build_edge_single(scene_t *s) {
+    obj_t **list = o_array(s, 1);
+    list[0] = o_sphere(s, V(0, 1, 0), 1, m_lambert(s, t_const(s, 0.5, 0.5, 0.5)));
+    return o_list(s, list, 1);
+}
+static obj_t *build_edge_degenerate(scene_t *s) {
+    obj_t **list = o_array(s, 11);
+    int i = 0;
+    mat_t *glass = m_dielectric(s, 1.5);
+    list[i++] = o_sphere(s, V(0, -1000, 0), 1000, m_lambert(s, t_const(s, 0.5, 0.5, 0.5)));
+    list[i++] = o_sphere(s, V(0, 1, 0), 0, m_lambert(s, t_const(s, 0.8, 0.3, 0.3)));
+    list[i++] = o_sphere(s, V(-2.5f, 1, 0), -1, glass);
+    list[i++] = o_sphere(s, V(2.5f, 1, 0), 1, glass);
+    list[i++] = o_sphere(s, V(2.5f, 1, 0), -0.9f, glass);
+    list[i++] = o_rect(s, OB_XZ, -1, -1, -1, 1, 0.5f, m_light(s, t_const(s, 4, 4, 4)));
+    list[i++] = o_msphere(s, V(1, 0.5f, 1.5f), V(1, 0.5f, 2), 0.5f, 0.5f, 0.5f, m_lambert(s, t_const(s, 0.2, 0.8, 0.2)));
+    list[i++] = o_sphere(s, V(-1, 0.7f, 1.5f), 0.7f, m_metal(s, V(0.7f, 0.6f, 0.5f), 1.5f));
+    list[i++] = o_medium(s, o_sphere(s, V(1, 0.5f, -1.5f), 0.5f, glass), 0, t_const(s, 1, 1, 1));
+    list[i++] = o_medium(s, o_sphere(s, V(-1, 0.5f, -1.5f), 0.5f, glass), 1e30f, t_const(s, 0.9, 0.9, 0.9));
+    list[i++] = o_flip(s, o_rect(s, OB_XY, -3, 3, 0, 3, -3, m_light(s, t_const(s, 2, 2, 2))));
+    return o_list(s, list, i);
+}
+
 static void collect_media(scene_t *s, obj_t *o) {
     switch (o->kind) {
     case OB_LIST: for (int i = 0; i < o->nkids; i++) collect_media(s, o->kids[i]); break;
@@ -686,6 +711,9 @@ static int scene_build(scene_t *s, int which, rng_t *g_after) {
     case ORACLE_SCENE_TWO_SPHERES: s->world = build_two_spheres(s); break;
     case ORACLE_SCENE_TEST: s->world = build_test(s); break;
     case ORACLE_SCENE_EARTH: if (!g_image) return -1; s->world = build_earth(s); break;
+    case ORACLE_SCENE_EDGE_EMPTY: s->world = build_edge_empty(s); break;
+    case ORACLE_SCENE_EDGE_SINGLE: s->world = build_edge_single(s); break;
+    case ORACLE_SCENE_EDGE_DEGENERATE: s->world = build_edge_degenerate(s); break;
     default: return -1;
     }
     collect_media(s, s->world);

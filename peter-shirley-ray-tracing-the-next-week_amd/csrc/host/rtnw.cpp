@@ -391,6 +391,37 @@ hitable *earth(const char *png_path) {   // main.cpp:87-97
     return new hitable_list(list, 2);
 }
 
+// Edge scenes of the tests (not in the reference's main.cpp), the same objects as
+// oracle/ref_harness.cpp edge_* builds from the reference's classes: no objects;
+// one sphere (a BVH that is a single leaf); degenerate geometry.
+hitable *edge_empty() { return new hitable_list(new hitable *[1], 0); }
+
+hitable *edge_single() {
+    hitable **l = new hitable *[1];
+    l[0] = new sphere(vec3(0, 1, 0), 1, new lambertian(new constant_texture(vec3(0.5, 0.5, 0.5))));
+    return new hitable_list(l, 1);
+}
+
+hitable *edge_degenerate() {
+    hitable **l = new hitable *[11];
+    int i = 0;
+    material *glass = new dielectric(1.5);
+    l[i++] = new sphere(vec3(0, -1000, 0), 1000, new lambertian(new constant_texture(vec3(0.5, 0.5, 0.5))));
+    l[i++] = new sphere(vec3(0, 1, 0), 0, new lambertian(new constant_texture(vec3(0.8, 0.3, 0.3))));   // zero radius
+    l[i++] = new sphere(vec3(-2.5, 1, 0), -1, glass);                                                  // negative radius
+    l[i++] = new sphere(vec3(2.5, 1, 0), 1, glass);                                                    // hollow bubble
+    l[i++] = new sphere(vec3(2.5, 1, 0), -0.9, glass);
+    l[i++] = new xz_rect(-1, -1, -1, 1, 0.5, new diffuse_light(new constant_texture(vec3(4, 4, 4))));   // zero width
+    l[i++] = new moving_sphere(vec3(1, 0.5, 1.5), vec3(1, 0.5, 2), 0.5, 0.5, 0.5,                        // zero shutter span
+                               new lambertian(new constant_texture(vec3(0.2, 0.8, 0.2))));
+    l[i++] = new sphere(vec3(-1, 0.7, 1.5), 0.7, new metal(vec3(0.7, 0.6, 0.5), 1.5));                  // fuzz clamped to 1
+    l[i++] = new constant_medium(new sphere(vec3(1, 0.5, -1.5), 0.5, glass), 0, new constant_texture(vec3(1, 1, 1)));
+    l[i++] = new constant_medium(new sphere(vec3(-1, 0.5, -1.5), 0.5, glass), 1e30,
+                                 new constant_texture(vec3(0.9, 0.9, 0.9)));
+    l[i++] = new flip_normals(new xy_rect(-3, 3, 0, 3, -3, new diffuse_light(new constant_texture(vec3(2, 2, 2)))));
+    return new hitable_list(l, i);
+}
+
 hitable *build_named_scene(const std::string &name, float *time0, float *time1) {
     reset_reference_rng();
     *time0 = 0.0f;
@@ -403,6 +434,9 @@ hitable *build_named_scene(const std::string &name, float *time0, float *time1) 
     if (name == "simple_light") return simple_light();
     if (name == "two_spheres") return two_spheres();
     if (name == "test") return test_scene();
+    if (name == "edge_empty") return edge_empty();
+    if (name == "edge_single") return edge_single();
+    if (name == "edge_degenerate") return edge_degenerate();
     if (name == "earth") {
         const char *png = std::getenv("RTNW_EARTH_PNG");
         return earth(png ? png : "picture.png");

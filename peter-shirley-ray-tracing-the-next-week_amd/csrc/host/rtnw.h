@@ -397,6 +397,9 @@ std::string dump_desc(const rt_scene_desc *d);
 hitable *random_scene();         // main.cpp:49-85
 hitable *random_scene_motion();  // TNW/Chapter01:36-67 with the main.cpp texture API
 hitable *two_spheres();          // main.cpp:99-110
+hitable *edge_empty();           // the tests' edge scenes (oracle/ref_harness.cpp edge_*)
+hitable *edge_single();
+hitable *edge_degenerate();
 hitable *simple_light();         // main.cpp:122-133
 hitable *test_scene();           // main.cpp:135-145 (`test`)
 hitable *cornell_box();          // main.cpp:148-166

@@ -194,6 +194,9 @@ SCENE_DEFAULTS = {   # per-scene camera / background / depth pairing (SURVEY §8
     "final": ("cornell", RT_BG_BLACK, 50),
     "simple_light": ("random", RT_BG_BLACK, 50),
     "two_spheres": ("random", RT_BG_BLACK, 50),
+    "edge_empty": ("random", RT_BG_SKY, 50),        # the tests' edge scenes (oracle/ref_harness.cpp edge_*)
+    "edge_single": ("random", RT_BG_SKY, 50),
+    "edge_degenerate": ("random", RT_BG_SKY, 50),
     "test": ("random", RT_BG_BLACK, 50),
     "earth": ("cornell", RT_BG_BLACK, 50),
 }

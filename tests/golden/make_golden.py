@@ -30,6 +30,7 @@ CANONICAL = [
     ("final", 40, 40, 4), ("final", 100, 100, 10), ("random_scene", 200, 100, 10), ("cornell_box", 40, 40, 8),
     ("cornell_smoke", 32, 32, 4), ("random_motion", 40, 20, 4), ("simple_light", 40, 20, 4),
     ("two_spheres", 20, 20, 4), ("test", 20, 20, 4), ("earth", 40, 40, 8),
+    ("edge_empty", 20, 10, 2), ("edge_single", 40, 20, 4), ("edge_degenerate", 40, 20, 8),
 ]
 # counter-RNG reference framebuffers: (name, scene, nx, ny, ns, seed)
 COUNTER = [
@@ -37,6 +38,8 @@ COUNTER = [
     ("c3_motion", "random_motion", 40, 20, 4, 3), ("c4_final", "final", 24, 24, 8, 4),
     ("smoke", "cornell_smoke", 24, 24, 8, 5), ("simple_light", "simple_light", 32, 16, 4, 6),
     ("earth", "earth", 32, 32, 8, 7),
+    ("edge_empty", "edge_empty", 16, 8, 2, 12), ("edge_single", "edge_single", 32, 16, 8, 13),
+    ("edge_degenerate", "edge_degenerate", 40, 20, 8, 14),
 ]
 
 

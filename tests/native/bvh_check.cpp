@@ -113,7 +113,9 @@ int check(const char *name, const rt_prim *prims, int n, const rt_instance *inst
         const rtnw::BvhResult r = rtnw::build_bvh(prims, n, inst, t0, t1);
         Checker c{prims, n, r, std::vector<int>(n, 0), ""};
         int bound = 0;
-        if (r.root & RT_LEAF_BIT) {   // a single-leaf scene: the leaf is the root
+        if (n == 0) {   // no primitives: no tree (the scene renders with has_bvh = 0)
+            if (!r.nodes2.empty() || !r.nodes4.empty() || !r.order.empty()) c.err = "a tree for an empty scene";
+        } else if (r.root & RT_LEAF_BIT) {   // a single-leaf scene: the leaf is the root
             const float lo[3] = {-INFINITY, -INFINITY, -INFINITY}, hi[3] = {INFINITY, INFINITY, INFINITY};
             c.child(width, r.root, lo, hi, 0);
             if (!(width == 2 ? r.nodes2.empty() : r.nodes4.empty())) c.err = "nodes emitted for a single-leaf scene";
@@ -145,7 +147,7 @@ int main() {
     setvbuf(stdout, nullptr, _IONBF, 0);
     int bad = 0;
     const char *names[] = {"final", "random_scene", "cornell_box", "cornell_smoke", "random_motion", "simple_light",
-                           "test", "two_spheres"};
+                           "test", "two_spheres", "edge_empty", "edge_single", "edge_degenerate"};
     for (const char *nm : names) {
         rt_scene_desc *d = nullptr;
         if (rt_builtin_scene_desc(nm, &d) != 0) { std::printf("%s: %s\n", nm, rt_last_error()); return 2; }

@@ -65,6 +65,10 @@ CASES = [   # (scene, nx, ny, spp, chunk, seed)  — c1..c4 of BASELINE.json at 
     ("test", 32, 16, 8, 3, 7),
     ("two_spheres", 24, 24, 4, 4, 8),
     ("earth", 32, 32, 8, 8, 9),
+    # edge cases (oracle pinned to the reference on them: tests/golden ref_edge_*)
+    ("edge_empty", 16, 8, 2, 2, 10),        # no objects: no BVH, every ray is background
+    ("edge_single", 32, 16, 8, 8, 11),      # one sphere: the BVH root is a leaf
+    ("edge_degenerate", 40, 20, 16, 16, 12),   # zero/negative radii, zero-width rect, 0/0 shutter, density 0 and 1e30
 ]
 
 
@@ -81,8 +85,38 @@ def test_gpu_matches_oracle(scene, nx, ny, ns, chunk, seed):
     assert exact > 0.5
 
 
+EDGE_PARAMS = [   # (scene, nx, ny, spp, chunk, max_depth, background, t_min)
+    ("final", 1, 1, 1, 1, 50, None, 0.001),              # one pixel, one sample
+    ("cornell_box", 17, 9, 3, 2, 0, None, 0.001),        # max_depth 0: emission only, never a scatter
+    ("cornell_smoke", 13, 7, 4, 3, 1, None, 0.001),      # a single bounce, media included
+    ("random_scene", 31, 3, 5, 7, 50, "black", 0.001),   # chunk > spp; black background on a sky scene
+    ("two_spheres", 9, 9, 4, 4, 50, "sky", 0.0),         # t_min 0: self-intersections, as the reference would
+    ("edge_degenerate", 23, 13, 6, 5, 3, None, 0.25),    # a large t_min on degenerate geometry
+]
+
+
+@pytest.mark.parametrize("scene,nx,ny,ns,chunk,depth,bg,tmin", EDGE_PARAMS)
+def test_gpu_matches_oracle_at_parameter_edges(scene, nx, ny, ns, chunk, depth, bg, tmin):
+    """Render-parameter edge cases through the C ABI, against the oracle's statement
+    of the kernel with the same parameters (main.cpp:27 t_min, :34 depth, :44 miss)."""
+    cam_name, bg0, _ = rtnw.SCENE_DEFAULTS[scene]
+    bgv = bg0 if bg is None else (rtnw.RT_BG_SKY if bg == "sky" else rtnw.RT_BG_BLACK)
+    p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bgv, chunk=chunk, seed=21, t_min=tmin)
+    g = _scene(scene).render_tile(rtnw.Camera.preset(cam_name, nx, ny), p, 0, 0, nx, ny)
+    o = O.render(O.kernel_spec(scene, nx, ny, ns, seed=21, chunk=chunk, max_depth=depth, tmin=tmin,
+                               background=None if bg is None else bg, threads=THREADS))[0]
+    assert g.shape == o.shape == (ny, nx, 3)
+    assert np.isfinite(g).all() and (g >= 0).all()
+    rms = gamma_rms(g, o)
+    exact = np.mean(g.view(np.uint32) == o.view(np.uint32))
+    print(f"{scene} depth {depth} t_min {tmin}: gamma RMS {rms}, bit-exact fraction {exact:.4f}")
+    assert (rms <= TOL_RMS).all(), rms
+    if depth == 0:   # emission only: no transcendental on the path, so every pixel agrees
+        assert exact == 1.0
+
+
 @pytest.mark.parametrize("name", ["c1_random", "c2_cornell", "c3_motion", "c4_final", "smoke", "simple_light",
-                                  "earth"])
+                                  "earth", "edge_empty", "edge_single", "edge_degenerate"])
 def test_gpu_matches_reference_framebuffer(golden, name):
     """Against the reference's own counter-RNG output (golden, made by the reference binary)."""
     c = golden["counter_fb"][name]
@@ -199,7 +233,9 @@ def test_ppm_from_gpu_mean_matches_oracle_quantiser():
 
 
 @pytest.mark.parametrize("scene,nx,ny,ns", [("final", 48, 48, 16), ("cornell_smoke", 32, 32, 8),
-                                            ("random_motion", 40, 20, 8), ("earth", 32, 32, 8)])
+                                            ("random_motion", 40, 20, 8), ("earth", 32, 32, 8),
+                                            ("edge_empty", 16, 8, 2), ("edge_single", 24, 12, 4),
+                                            ("edge_degenerate", 40, 20, 8)])
 def test_engines_and_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     """The megakernel and the workgroup-wavefront engine (RTNW_ENGINE=wave) run the same
     per-sample arithmetic and sum each work item in sample order, and the closest hit is
