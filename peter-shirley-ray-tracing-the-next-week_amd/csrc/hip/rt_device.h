@@ -677,6 +677,34 @@ __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec
     return res;
 }
 
+// ----------------------------------------------------------------- camera
+// camera.h:41-56's state, kept in LDS and read (volatile: once per use, not hoisted)
+// by the camera stage: held in SGPRs across the persistent loop, its 24 floats
+// pushed the kernel past the SGPR limit and came back as per-iteration v_readlanes.
+typedef float CamV4 __attribute__((ext_vector_type(4)));
+struct CamView { V3 llc, hor, ver, org, cu, cv; float t0, t1, lens; };
+__device__ __forceinline__ void store_camera(const RtKernelArgs &A, CamV4 *lds) {
+    lds[0] = CamV4{A.llc[0], A.llc[1], A.llc[2], A.ct0};
+    lds[1] = CamV4{A.hor[0], A.hor[1], A.hor[2], A.ct1};
+    lds[2] = CamV4{A.ver[0], A.ver[1], A.ver[2], A.lens};
+    lds[3] = CamV4{A.org[0], A.org[1], A.org[2], 0.f};
+    lds[4] = CamV4{A.cu[0], A.cu[1], A.cu[2], 0.f};
+    lds[5] = CamV4{A.cv[0], A.cv[1], A.cv[2], 0.f};
+}
+typedef __attribute__((address_space(3))) const volatile CamV4 LdsCamV4;   // keeps ds_read (not flat)
+__device__ __forceinline__ CamView load_camera(const CamV4 *lds) {
+    const LdsCamV4 *v = (const LdsCamV4 *)lds;
+    const CamV4 a = v[0], b = v[1], c = v[2], d = v[3], e = v[4], f = v[5];
+    CamView C;
+    C.llc = mk(a.x, a.y, a.z); C.t0 = a.w;
+    C.hor = mk(b.x, b.y, b.z); C.t1 = b.w;
+    C.ver = mk(c.x, c.y, c.z); C.lens = c.w;
+    C.org = mk(d.x, d.y, d.z);
+    C.cu = mk(e.x, e.y, e.z);
+    C.cv = mk(f.x, f.y, f.z);
+    return C;
+}
+
 // ------------------------------------------------------------------ media
 // constant_medium::hit for every medium after the surface search
 // (constant_medium.h:26-50): the boundary's entry/exit, clipped to [t_min, best]
@@ -705,67 +733,86 @@ __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds
     }
 }
 
+// One medium's test (constant_medium.h:26-50) against the surface result.
+template <bool kCount>
+__device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, int depth,
+                                           const Rng &g, bool &have, float &best_t, int &med_mat, Counters &cnt) {
+    if (kCount) cnt.media++;
+    const int4 md = M.md;
+    float r1, r2;
+    bool ok;
+    const float4 bm = M.mm;
+    if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {   // wave-uniform
+        // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
+        if (kCount) cnt.spheres++;
+        const float4 sg = M.g0;
+        V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
+        float a = dot(r.d, r.d);
+        float b = dot(oc, r.d);
+        float cc = dot(oc, oc) - sg.w * sg.w;
+        float disc = b * b - a * cc;
+        const bool valid = disc > 0;
+        if (__ballot(valid) == 0ull) return;   // the whole wave misses the boundary
+        const float sq = sqrtf(disc);
+        const float ta = (-b - sq) / a;
+        const float tb = (-b + sq) / a;
+        // selects, not branches: sphere.h:33-44 for t_min = -FLT_MAX, then t_min = r1 + 0.0001
+        const bool fa = ta < RT_FLT_MAX && ta > -RT_FLT_MAX, fb = tb < RT_FLT_MAX && tb > -RT_FLT_MAX;
+        r1 = fa ? ta : tb;
+        const float tmin2 = (float)((double)r1 + 0.0001);
+        const bool ga = ta < RT_FLT_MAX && ta > tmin2, gb = tb < RT_FLT_MAX && tb > tmin2;
+        r2 = ga ? ta : tb;
+        ok = valid && (fa || fb) && (ga || gb);
+    } else {
+        r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
+        ok = r1 != RT_INF;
+        if (__ballot(ok) == 0ull) return;
+        r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
+        ok = ok && r2 != RT_INF;
+    }
+    const float tmax = have ? best_t : RT_FLT_MAX;
+    r1 = r1 < A.tmin ? A.tmin : r1;
+    r2 = r2 > tmax ? tmax : r2;
+    ok = ok && !(r1 >= r2);
+    if (__ballot(ok) == 0ull) return;   // no lane inside the medium: no free-flight draw
+    r1 = r1 < 0 ? 0.f : r1;
+    const float dlen = len(r.d);
+    const float distance_inside_boundary = (r2 - r1) * dlen;
+    const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
+    const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k)));
+    const bool hit = ok && hit_distance < distance_inside_boundary;
+    const float tm = r1 + hit_distance / dlen;
+    best_t = hit ? tm : best_t;
+    have = have || hit;
+    med_mat = hit ? md.w : med_mat;
+}
+
+// All media in list order.  The first RT_LDS_MEDIA come from the workgroup's LDS
+// copy through an explicit LDS pointer, the rest from HBM, in two loops: one loop
+// choosing per medium between the two made the compiler select the address and
+// issue generic (flat) loads, which wait on both memory counters.
 template <bool kCount>
 __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, int depth,
                                          const Rng &g, bool &have, float &best_t, Counters &cnt) {
+    typedef unsigned U4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const U4v LdsU4;
     int med_mat = -1;
-    for (int k = 0; k < A.nmedia; ++k) {
-        if (kCount) cnt.media++;
+    const int nl = min(A.nmedia, RT_LDS_MEDIA);
+    for (int k = 0; k < nl; ++k) {
+        const LdsU4 *p = (const LdsU4 *)lds_media + 3 * k;
+        const U4v x = p[0], y = p[1], z = p[2];
         MediumRec M;
-        if (k < RT_LDS_MEDIA) {
-            M = lds_media[k];
-        } else {
-            M.md = A.media[k];
-            M.g0 = A.bprims[M.md.x * 4 + 0];
-            M.mm = A.bprims[M.md.x * 4 + 1];
-        }
-        const int4 md = M.md;
-        float r1, r2;
-        bool ok;
-        const float4 bm = M.mm;
-        if (md.y == 1 && (fbits(bm.x) & 0xff) == RT_PRIM_SPHERE && fbits(bm.z) < 0) {   // wave-uniform
-            // one sphere: both boundary calls (constant_medium.h:28-29) share the roots
-            if (kCount) cnt.spheres++;
-            const float4 sg = M.g0;
-            V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
-            float a = dot(r.d, r.d);
-            float b = dot(oc, r.d);
-            float cc = dot(oc, oc) - sg.w * sg.w;
-            float disc = b * b - a * cc;
-            const bool valid = disc > 0;
-            if (__ballot(valid) == 0ull) continue;   // the whole wave misses the boundary
-            const float sq = sqrtf(disc);
-            const float ta = (-b - sq) / a;
-            const float tb = (-b + sq) / a;
-            // selects, not branches: sphere.h:33-44 for t_min = -FLT_MAX, then t_min = r1 + 0.0001
-            const bool fa = ta < RT_FLT_MAX && ta > -RT_FLT_MAX, fb = tb < RT_FLT_MAX && tb > -RT_FLT_MAX;
-            r1 = fa ? ta : tb;
-            const float tmin2 = (float)((double)r1 + 0.0001);
-            const bool ga = ta < RT_FLT_MAX && ta > tmin2, gb = tb < RT_FLT_MAX && tb > tmin2;
-            r2 = ga ? ta : tb;
-            ok = valid && (fa || fb) && (ga || gb);
-        } else {
-            r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
-            ok = r1 != RT_INF;
-            if (__ballot(ok) == 0ull) continue;
-            r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
-            ok = ok && r2 != RT_INF;
-        }
-        const float tmax = have ? best_t : RT_FLT_MAX;
-        r1 = r1 < A.tmin ? A.tmin : r1;
-        r2 = r2 > tmax ? tmax : r2;
-        ok = ok && !(r1 >= r2);
-        if (__ballot(ok) == 0ull) continue;   // no lane inside the medium: no free-flight draw
-        r1 = r1 < 0 ? 0.f : r1;
-        const float dlen = len(r.d);
-        const float distance_inside_boundary = (r2 - r1) * dlen;
-        const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
-        const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k)));
-        const bool hit = ok && hit_distance < distance_inside_boundary;
-        const float tm = r1 + hit_distance / dlen;
-        best_t = hit ? tm : best_t;
-        have = have || hit;
-        med_mat = hit ? md.w : med_mat;
+        M.md = make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
+        M.g0 = make_float4(__uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w));
+        M.mm = make_float4(__uint_as_float(z.x), __uint_as_float(z.y), __uint_as_float(z.z), __uint_as_float(z.w));
+        medium_one<kCount>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
+    }
+    for (int k = RT_LDS_MEDIA; k < A.nmedia; ++k) {
+        MediumRec M;
+        M.md = A.media[k];
+        M.g0 = A.bprims[M.md.x * 4 + 0];
+        M.mm = A.bprims[M.md.x * 4 + 1];
+        medium_one<kCount>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
     }
     return med_mat;
 }

@@ -60,11 +60,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
+    __shared__ CamV4 lds_cam[6];
     const uint32_t lane = lane_id();
     uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
     // the media records are read from LDS (one broadcast read per medium)
     load_media(A, lds_media);
+    if (threadIdx.x == 0) store_camera(A, lds_cam);
     __syncthreads();
 
     const uint64_t skey = seed_key(A.seed);   // per-launch part of the sample keys
@@ -160,13 +162,12 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         }
         const V3 disk = coop_reject<2, kCount>(starting, g, slots, lane, cnt, DiskCand());
         if (starting) {
-            V3 rd = scale(A.lens, disk);
-            V3 cu = mk(A.cu[0], A.cu[1], A.cu[2]), cv = mk(A.cv[0], A.cv[1], A.cv[2]);
-            V3 offset = add(scale(rd.x, cu), scale(rd.y, cv));
-            float time = (float)((double)A.ct0 + g.next() * (double)(A.ct1 - A.ct0));
-            V3 org = mk(A.org[0], A.org[1], A.org[2]);
-            V3 dir = sub(sub(add(add(mk(A.llc[0], A.llc[1], A.llc[2]), scale(cu_, mk(A.hor[0], A.hor[1], A.hor[2]))),
-                                 scale(cv_, mk(A.ver[0], A.ver[1], A.ver[2]))), org), offset);
+            const CamView C = load_camera(lds_cam);
+            V3 rd = scale(C.lens, disk);
+            V3 offset = add(scale(rd.x, C.cu), scale(rd.y, C.cv));
+            float time = (float)((double)C.t0 + g.next() * (double)(C.t1 - C.t0));
+            V3 org = C.org;
+            V3 dir = sub(sub(add(add(C.llc, scale(cu_, C.hor)), scale(cv_, C.ver)), org), offset);
             r.o = add(org, offset);
             r.d = dir;
             r.time = time;
