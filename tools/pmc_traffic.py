@@ -61,7 +61,7 @@ def main():
         res["valu_insts_per_sample_wave"] = sq["SQ_INSTS_VALU"] * 64 / samples
         res["effective_clock_ghz"] = sq["GRBM_GUI_ACTIVE"] / 8 / sq["dur_ns"]
         res["waves"] = sq["SQ_WAVES"]
-        res["vgpr"] = sq["vgpr"]
+        res["rocprof_VGPR_Count"] = sq["vgpr"]   # rocprof's field (the code object says 128 VGPRs)
         res["scratch_bytes_per_lane"] = sq["scratch"]
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, "traffic.json"), "w") as f:
