@@ -9,11 +9,12 @@ persistent HIP megakernel, plus (N > 1) the RCCL gather of the packed tiles to
 rank 0.  Scene upload and BVH build happen before the timed region (inputs
 resident in HBM); the PPM write is not part of a step.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling — N ranks render an image
-of N x 250,000 pixels (500x500, 1000x500, 1000x1000 = config 5's image, 2000x1000),
-32x32 tiles interleaved diagonally (tile (tx, ty) -> rank (tx + ty) % N), then one
-torch.distributed gather (backend "nccl" = RCCL over xGMI) of the packed float
-tiles to rank 0.  `--dist-backend gloo` gathers through host memory instead, so the
+Multi-GPU (torchrun, one process per GPU): weak scaling — N ranks render the same
+view at N x 250,000 pixels (square, side round(500 sqrt(N)): 500, 707, 1000 =
+config 5's image, 1414).  The pixels are interleaved over the ranks (N = a x b,
+rank (ry, rx) renders x = rx mod a, y = ry mod b: a sub-sampled copy of the whole
+view, so every rank's expected cost is the same), then one torch.distributed
+gather (backend "nccl" = RCCL over xGMI) of the packed float pixels to rank 0.  `--dist-backend gloo` gathers through host memory instead, so the
 multi-rank path can be rehearsed with several ranks on one GPU.
 
 Prints ONE JSON line (rank 0) with roofline (algorithmic bytes / kernel time vs
@@ -38,7 +39,8 @@ import torch.distributed as dist  # noqa: E402
 import rtnw  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TILE = 32
+TILE = 8                       # unused by the interleaved layout
+LAYOUT = "interleaved"         # rtnw.pixels_for_rank: rank (ry, rx) of a x b renders x = rx mod a, y = ry mod b
 
 
 def log(*a):
@@ -46,18 +48,12 @@ def log(*a):
 
 
 def image_for(n):
-    # N x 250k pixels: 500x500, 1000x500, 1000x1000, 2000x1000, ...
-    w, h = 500, 500
-    k = 1
-    while k < n:
-        if w <= h:
-            w *= 2
-        else:
-            h *= 2
-        k *= 2
-    if k != n:   # non power of two: stretch the width
-        w, h = 500 * n, 500
-    return w, h
+    """N x 250k pixels at the 1-GPU image's aspect and view: side round(500 sqrt(N))
+    (500, 707, 1000 = config 5's image, 1414).  A wider image would show more of
+    the dark ground and cost ~18% less per sample (tools/scaling_probe.py --fullres),
+    so per-GPU work would shrink with N."""
+    side = round(500 * n ** 0.5)
+    return side, side
 
 
 def cpu_baseline(budget_procs):
@@ -151,7 +147,7 @@ def main():
     nx, ny = image_for(world)
     spp = args.spp
     if world > 1:
-        all_tiles, all_counts = rtnw.rank_layout(nx, ny, TILE, world)
+        all_tiles, all_counts = rtnw.rank_layout(nx, ny, TILE, world, LAYOUT)
     else:
         all_tiles, all_counts = [[(0, 0, nx, ny)]], [nx * ny * 3]
     tiles = all_tiles[rank]
@@ -233,8 +229,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic: procedural final() scene (main.cpp:190-230), counter-RNG samples, seed 2024",
             "config": {"workload": workload, "image": [nx, ny], "spp": spp, "pixels_per_gpu": nx * ny // world,
-                       "tile": TILE if world > 1 else None, "chunk": args.chunk,
-                       "parallelism": f"pixel tiles x{world}" + (" + RCCL gather" if world > 1 else "")},
+                       "rank_layout": ("pixel interleave %dx%d" % rtnw.interleave_factors(world)) if world > 1 else None,
+                       "chunk": args.chunk,
+                       "parallelism": f"pixels x{world}" + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(len(tiles) and sum(w * h for _, _, w, h in tiles) * spp),
                          "kernel_ms_avg": avg_kernel_s * 1e3,

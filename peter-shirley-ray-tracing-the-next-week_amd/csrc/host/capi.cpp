@@ -374,8 +374,10 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     return RT_OK;
 }
 
-// Job pixel order: tiles in the order given; inside a tile, 8x8 pixel blocks so
-// that the 64 lanes of a wave start on neighbouring pixels (coherent primary rays).
+// Job pixel order: tiles in the order given; inside a tile, bands of 8 rows listed
+// column by column (8 pixels per column), so that ANY 64 consecutive items — a wave
+// claim, wherever it starts — are 8 neighbouring columns of one band (coherent
+// primary rays), also when the tile width is not a multiple of 8 (500 = 62.5 x 8).
 static int prepare_job(rt_scene *s, const int32_t *tiles, int ntiles, int nx, int ny) {
     std::vector<int32_t> key(tiles, tiles + 4 * ntiles);
     if (key == s->job_tiles && s->job_xy) return RT_OK;
@@ -386,12 +388,11 @@ static int prepare_job(rt_scene *s, const int32_t *tiles, int ntiles, int nx, in
         if (w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > nx || y0 + h > ny || nx > 65535 || ny > 65535)
             return fail(RT_ERR_INVALID, "tile outside the image");
         for (int by = 0; by < h; by += 8)
-            for (int bx = 0; bx < w; bx += 8)
-                for (int yy = by; yy < std::min(by + 8, h); yy++)
-                    for (int xx = bx; xx < std::min(bx + 8, w); xx++) {
-                        xy.push_back((uint32_t)(x0 + xx) | ((uint32_t)(y0 + yy) << 16));
-                        oi.push_back(base + (uint32_t)(yy * w + xx));
-                    }
+            for (int xx = 0; xx < w; xx++)
+                for (int yy = by; yy < std::min(by + 8, h); yy++) {
+                    xy.push_back((uint32_t)(x0 + xx) | ((uint32_t)(y0 + yy) << 16));
+                    oi.push_back(base + (uint32_t)(yy * w + xx));
+                }
         base += (uint32_t)(w * h);
     }
     if (s->job_xy) { (void)hipFree(s->job_xy); s->job_xy = nullptr; }

@@ -303,27 +303,84 @@ def ppm_text(rgb: np.ndarray) -> bytes:
     return buf.raw[:n]
 
 
-def tiles_for_rank(nx, ny, tile, rank, world):
-    """Diagonal interleave: tile (tx, ty) goes to rank (tx + ty) % world.  Neighbouring
-    tiles land on different ranks (spatially varying path cost evens out) and the
-    narrow edge tiles rotate over the ranks (pixel counts balance)."""
+def _mix64(z):
+    M = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
+
+
+def tiles_for_rank(nx, ny, tile, rank, world, order="diagonal"):
+    """Tiles of one rank, in raster order.
+    order="diagonal": tile (tx, ty) goes to rank (tx + ty) % world.  Neighbouring
+      tiles land on different ranks and the narrow edge tiles rotate over the ranks.
+    order="hashed": the tiles are ranked by a hash of their raster index and dealt
+      round-robin, so every rank holds the same number of tiles (+-1) scattered
+      uniformly over the image: its expected path cost is the image mean whatever
+      the scene's spatial structure (bench.py uses 8x8 tiles = one wave claim)."""
+    cols = (nx + tile - 1) // tile
+    rows = (ny + tile - 1) // tile
+    if order == "hashed":
+        ranked = sorted(range(cols * rows), key=lambda i: (_mix64(i ^ 0x243F6A8885A308D3), i))
+        mine = sorted(ranked[rank::world])
+    elif order == "diagonal":
+        mine = [ty * cols + tx for ty in range(rows) for tx in range(cols) if (tx + ty) % world == rank]
+    else:
+        raise ValueError(f"unknown tile order {order!r}")
     out = []
-    for ty, y0 in enumerate(range(0, ny, tile)):
-        for tx, x0 in enumerate(range(0, nx, tile)):
-            if (tx + ty) % world == rank:
-                out.append((x0, y0, min(tile, nx - x0), min(tile, ny - y0)))
+    for i in mine:
+        x0, y0 = (i % cols) * tile, (i // cols) * tile
+        out.append((x0, y0, min(tile, nx - x0), min(tile, ny - y0)))
     return out
 
 
-def rank_layout(nx, ny, tile, world):
-    """Tiles and packed float counts of every rank (interleaved assignment)."""
-    tiles = [tiles_for_rank(nx, ny, tile, r, world) for r in range(world)]
+def interleave_factors(world):
+    """world = a x b with a >= b as close to square as possible (8 -> 4 x 2)."""
+    b = int(world ** 0.5)
+    while world % b:
+        b -= 1
+    return world // b, b
+
+
+def pixels_for_rank(nx, ny, rank, world, block=8):
+    """Pixel interleave: with world = a x b, rank (ry, rx) = divmod(rank, a) renders
+    the pixels x = rx (mod a), y = ry (mod b) — a sub-sampled copy of the whole view,
+    so every rank's expected path cost is the image mean, whatever the scene's
+    spatial structure.  Returned as 1x1 tiles in the order of the rank's
+    sub-lattice: bands of `block` rows, each listed column by column, so ANY
+    64 consecutive pixels (one wave claim, wherever it starts) cover 8 neighbouring
+    columns of one band (two bands at a band's end)."""
+    a, b = interleave_factors(world)
+    ry, rx = divmod(rank, a)
+    xs = np.arange(rx, nx, a, dtype=np.int64)
+    ys = np.arange(ry, ny, b, dtype=np.int64)
+    if xs.size == 0 or ys.size == 0:
+        return np.zeros((0, 4), np.int32)
+    J, I = np.meshgrid(np.arange(ys.size), np.arange(xs.size), indexing="ij")
+    key = ((J // block) * xs.size + I) * block + J % block
+    o = np.argsort(key.ravel(), kind="stable")
+    t = np.ones((o.size, 4), np.int32)
+    t[:, 0] = xs[I.ravel()[o]]
+    t[:, 1] = ys[J.ravel()[o]]
+    return t
+
+
+def rank_layout(nx, ny, tile, world, order="diagonal"):
+    """Tiles and packed float counts of every rank."""
+    if order == "interleaved":
+        tiles = [pixels_for_rank(nx, ny, r, world) for r in range(world)]
+        return tiles, [len(t) * 3 for t in tiles]
+    tiles = [tiles_for_rank(nx, ny, tile, r, world, order) for r in range(world)]
     counts = [sum(w * h for _, _, w, h in t) * 3 for t in tiles]
     return tiles, counts
 
 
 def unpack_tiles(packed, tiles, img):
     """Scatters one rank's packed tiles (as rt_render_tiles writes them) into img [ny, nx, 3]."""
+    t = np.asarray(tiles, dtype=np.int64).reshape(-1, 4)
+    if t.size and (t[:, 2:] == 1).all():   # pixel layouts: one vectorised scatter
+        img[t[:, 1], t[:, 0]] = np.asarray(packed[: 3 * len(t)]).reshape(-1, 3)
+        return img
     off = 0
     for x0, y0, w, h in tiles:
         img[y0:y0 + h, x0:x0 + w] = np.asarray(packed[off:off + w * h * 3]).reshape(h, w, 3)

@@ -1,4 +1,5 @@
-"""Multi-rank path on CPU (gloo, world size 2): interleaved tile sharding, packed
+"""Multi-rank path on CPU (gloo, world size 2): rank sharding (the pixel interleave
+bench.py uses, and diagonal tiles), packed
 per-rank buffers padded to a common length, one collective gather to rank 0,
 unpack on the root.  The per-tile renderer here is the oracle's statement of the
 kernel (the same per-pixel values the GPU produces; tests/test_gpu_parity.py
@@ -27,9 +28,14 @@ def _free_port():
     return p
 
 
-def render_rank(rank, world):
-    tiles, counts = rtnw.rank_layout(NX, NY, TILE, world)
+def render_rank(rank, world, order):
+    tiles, counts = rtnw.rank_layout(NX, NY, TILE, world, order)
     buf = np.zeros(max(counts), np.float32)
+    if order == "interleaved":   # 1x1 tiles: this rank's pixels of the (order-independent) image
+        full, _ = O.render(O.kernel_spec("final", NX, NY, NS, seed=SEED))
+        t = tiles[rank]
+        buf[: 3 * len(t)] = full[t[:, 1], t[:, 0]].reshape(-1)
+        return buf, tiles, counts
     off = 0
     for (x0, y0, w, h) in tiles[rank]:
         m, _ = O.render(O.kernel_spec("final", NX, NY, NS, seed=SEED, rect=(x0, y0, w, h)))
@@ -38,10 +44,10 @@ def render_rank(rank, world):
     return buf, tiles, counts
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, order, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    buf, tiles, counts = render_rank(rank, world)
+    buf, tiles, counts = render_rank(rank, world, order)
     t = torch.from_numpy(buf)
     gl = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
     dist.gather(t, gl, dst=0)
@@ -54,12 +60,12 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_gather_equals_single_rank_image(world):
+@pytest.mark.parametrize("world,order", [(2, "interleaved"), (2, "diagonal")])
+def test_gloo_gather_equals_single_rank_image(world, order):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, order, q)) for r in range(world)]
     for p in procs:
         p.start()
     img = q.get(timeout=300)
@@ -70,9 +76,28 @@ def test_gloo_gather_equals_single_rank_image(world):
     assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
 
 
-def test_layout_balances_ranks():
-    for world in (2, 4, 8):
-        nx, ny = {2: (1000, 500), 4: (1000, 1000), 8: (2000, 1000)}[world]
-        _, counts = rtnw.rank_layout(nx, ny, 32, world)
+@pytest.mark.parametrize("order", ["interleaved", "diagonal", "hashed"])
+def test_layout_covers_image_once_and_balances_ranks(order):
+    import bench
+    for world in (2, 3, 4, 8):
+        nx, ny = bench.image_for(world)
+        tiles, counts = rtnw.rank_layout(nx, ny, 8, world, order)
         assert sum(counts) == nx * ny * 3
         assert max(counts) / min(counts) < 1.02
+        cover = np.zeros((ny, nx), np.int32)
+        for t in tiles:
+            for x0, y0, w, h in np.asarray(t).reshape(-1, 4).tolist():
+                cover[y0:y0 + h, x0:x0 + w] += 1
+        assert (cover == 1).all(), (order, world)
+
+
+def test_interleave_claims_are_local():
+    """64 consecutive pixels of a rank (one wave claim) mostly stay within an 8x8
+    block of its sub-lattice, i.e. an 8a x 8b window of the image (a partial block
+    at the sub-lattice's right edge shifts the claims that follow it)."""
+    for world in (2, 4, 8):
+        a, b = rtnw.interleave_factors(world)
+        t = rtnw.pixels_for_rank(1000, 1000, world - 1, world)
+        local = [np.ptp(g[:, 0]) < 8 * a and np.ptp(g[:, 1]) < 16 * b
+                 for g in (t[k:k + 64] for k in range(0, len(t) - 64, 64))]
+        assert np.mean(local) > 0.9, (world, np.mean(local))

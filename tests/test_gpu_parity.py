@@ -137,7 +137,8 @@ def test_tile_decomposition_is_bitwise_invariant():
 
 
 def test_rank_sharding_gathers_to_single_gpu_image():
-    """Interleaved 16x16 tiles over R emulated ranks, packed per rank as the
+    """Rank layouts (16x16 tiles diagonal or hashed, the pixel interleave) over R
+    emulated ranks, packed per rank as the
     multi-GPU path sends them, unpacked on the root == the 1-rank image."""
     import ctypes
     nx, ny, ns = 80, 48, 4
@@ -147,11 +148,13 @@ def test_rank_sharding_gathers_to_single_gpu_image():
     p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, seed=5)
     sc = _scene("cornell_box")
     L = rtnw.lib()
-    for R in (2, 3, 8):
+    for R, order in ((2, "diagonal"), (3, "diagonal"), (8, "diagonal"), (2, "interleaved"), (8, "interleaved"),
+                     (3, "hashed")):
         img = np.zeros_like(full)
+        layout, _ = rtnw.rank_layout(nx, ny, 16, R, order)
         for r in range(R):
-            tiles = rtnw.tiles_for_rank(nx, ny, 16, r, R)
-            n = sum(w * h for _, _, w, h in tiles) * 3
+            tiles = layout[r]
+            n = sum(w * h for _, _, w, h in np.asarray(tiles).reshape(-1, 4).tolist()) * 3
             if n == 0:   # more ranks than tiles on this diagonal: nothing to render
                 assert sc.render_tiles(cam, p, [], 0)["samples"] == 0
                 continue
@@ -161,11 +164,8 @@ def test_rank_sharding_gathers_to_single_gpu_image():
             packed = np.zeros(n, np.float32)
             assert L.rt_copy_to_host(packed.ctypes.data, dev, n * 4) == 0
             L.rt_device_free(dev)
-            off = 0
-            for x0, y0, w, h in tiles:
-                img[y0:y0 + h, x0:x0 + w] = packed[off:off + w * h * 3].reshape(h, w, 3)
-                off += w * h * 3
-        assert np.array_equal(img.view(np.uint32), full.view(np.uint32)), R
+            rtnw.unpack_tiles(packed, tiles, img)
+        assert np.array_equal(img.view(np.uint32), full.view(np.uint32)), (R, order)
 
 
 def test_deterministic_across_launches():
