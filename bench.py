@@ -40,6 +40,7 @@ import rtnw  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 TILE = 8                       # unused by the interleaved layout
+METRIC = "Msamples/s (pixels×spp/s) + achieved HBM GB/s, final() 500×500×1000spp"   # BASELINE.json
 LAYOUT = "interleaved"         # rtnw.pixels_for_rank: rank (ry, rx) of a x b renders x = rx mod a, y = ry mod b
 
 
@@ -47,39 +48,59 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def image_for(n):
-    """N x 250k pixels at the 1-GPU image's aspect and view: side round(500 sqrt(N))
-    (500, 707, 1000 = config 5's image, 1414).  A wider image would show more of
-    the dark ground and cost ~18% less per sample (tools/scaling_probe.py --fullres),
-    so per-GPU work would shrink with N."""
-    side = round(500 * n ** 0.5)
-    return side, side
+# BASELINE.json configs on one GPU: scene, image, spp (depth / background / camera:
+# rtnw.SCENE_DEFAULTS).  c4 is the metric's config and the default; c2 and c3 are
+# reported with --config for DESIGN.md, never as the headline.
+CONFIGS = {
+    "c2": ("cornell_box", 400, 400, 200),
+    "c3": ("random_motion", 800, 400, 500),
+    "c4": ("final", 500, 500, 1000),
+}
 
 
-def cpu_baseline(budget_procs):
+def image_for(n, w=500, h=500):
+    """N x (w x h) pixels at the 1-GPU image's aspect and view: sides scaled by sqrt(N)
+    (final(): 500, 707, 1000 = config 5's image, 1414).  A wider image would show more
+    of the dark ground and cost ~18% less per sample (tools/scaling_probe.py
+    --fullres), so per-GPU work would shrink with N."""
+    k = n ** 0.5
+    return round(w * k), round(h * k)
+
+
+def cpu_baseline(budget_procs, scene_name, nx, ny, target_s=8.0):
     """Reference renderer (oracle/_ref/ref_render, compiled from the reference's own
-    sources) on host cores: final() 500x500 at 2 spp, rows split over P processes."""
+    sources) on host cores, rows split over P processes: a 1-spp pass calibrates the
+    sample count so the timed pass takes about `target_s` seconds."""
     ref = os.path.join(ORACLE, "_ref", "ref_render")
-    nx, ny, ns = 500, 500, 2
     P = budget_procs
+    cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
     if os.path.exists(ref) and os.access(ref, os.X_OK):
-        bands = [(ny * i // P, ny * (i + 1) // P) for i in range(P)]
-        t0 = time.perf_counter()
-        procs = [subprocess.Popen([ref, "--scene", "final", "--nx", str(nx), "--ny", str(ny), "--ns", str(ns),
-                                   "--rows", f"{a}:{b}"], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                                  cwd="/tmp") for a, b in bands]
-        rc = [p.wait() for p in procs]
-        dt = time.perf_counter() - t0
-        if all(r == 0 for r in rc):
-            return {"value": nx * ny * ns / dt / 1e6, "unit": "Msamples/s", "cores": P, "kind": "reference",
-                    "sample": f"final() {nx}x{ny}x{ns}spp, flat list as shipped (main.cpp:291), rows split over "
-                              f"{P} processes of oracle/_ref/ref_render (clang++ -O2), wall {dt:.2f}s"}
+        def run(ns):
+            bands = [(ny * i // P, ny * (i + 1) // P) for i in range(P)]
+            t0 = time.perf_counter()
+            procs = [subprocess.Popen([ref, "--scene", scene_name, "--nx", str(nx), "--ny", str(ny), "--ns", str(ns),
+                                       "--depth", str(depth), "--bg", "sky" if bg == rtnw.RT_BG_SKY else "black",
+                                       "--cam", cam_name, "--rows", f"{a}:{b}"],
+                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd="/tmp")
+                     for a, b in bands]
+            ok = all(p.wait() == 0 for p in procs)
+            return ok, time.perf_counter() - t0
+        ok, dt1 = run(1)
+        if ok:
+            ns = max(1, min(1000, round(target_s / max(dt1, 1e-3))))
+            ok, dt = run(ns)
+            if ok:
+                return {"value": nx * ny * ns / dt / 1e6, "unit": "Msamples/s", "cores": P, "kind": "reference",
+                        "sample": f"{scene_name}() {nx}x{ny}x{ns}spp (spp sized by a 1-spp pass), the reference's "
+                                  f"own accelerator choice (final(): flat list as shipped, main.cpp:291), rows split "
+                                  f"over {P} processes of oracle/_ref/ref_render (clang++ -O2), wall {dt:.2f}s"}
     sys.path.insert(0, ORACLE)
     import oracle as O
-    spec = O.kernel_spec("final", nx, ny, ns, seed=0, threads=P)
+    ns = 2
+    spec = O.kernel_spec(scene_name, nx, ny, ns, seed=0, threads=P)
     _, st = O.render(spec)
     return {"value": st["samples"] / st["seconds"] / 1e6, "unit": "Msamples/s", "cores": P, "kind": "port",
-            "sample": f"final() {nx}x{ny}x{ns}spp, oracle/rt_oracle.c flat list, OpenMP {P} threads, "
+            "sample": f"{scene_name}() {nx}x{ny}x{ns}spp, oracle/rt_oracle.c, OpenMP {P} threads, "
                       f"{st['seconds']:.2f}s"}
 
 
@@ -100,14 +121,14 @@ def read_traffic(samples_per_launch):
         return None
 
 
-def end_to_end(cam, params, nx, ny, dev):
+def end_to_end(scene_name, cam, params, nx, ny, dev):
     """SURVEY §8d's second reading of the metric: one more render of the same
     workload timed from scene creation (flatten, SAH build, upload to HBM) through
     the render to the framebuffer in host memory.  Reported beside `value`, never as
     it (`value` starts with the scene resident)."""
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    scene = rtnw.Scene.builtin("final", device=dev.index)
+    scene = rtnw.Scene.builtin(scene_name, device=dev.index)
     t1 = time.perf_counter()
     out = torch.empty(nx * ny * 3, dtype=torch.float32, device=dev)
     scene.render_tiles(cam, params, [(0, 0, nx, ny)], out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
@@ -127,7 +148,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=1000)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=0, help="override the config's spp")
     ap.add_argument("--chunk", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ppm", default="")
@@ -144,8 +166,10 @@ def main():
         dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", gpu)
 
-    nx, ny = image_for(world)
-    spp = args.spp
+    scene_name, w1, h1, spp = CONFIGS[args.config]
+    spp = args.spp or spp
+    cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
+    nx, ny = image_for(world, w1, h1)
     if world > 1:
         all_tiles, all_counts = rtnw.rank_layout(nx, ny, TILE, world, LAYOUT)
     else:
@@ -153,9 +177,9 @@ def main():
     tiles = all_tiles[rank]
     n_max = max(all_counts)
 
-    scene = rtnw.Scene.builtin("final", device=gpu)
-    cam = rtnw.Camera.preset("cornell", nx, ny)
-    params = rtnw.RenderParams(nx, ny, spp, max_depth=50, chunk=args.chunk, seed=2024)
+    scene = rtnw.Scene.builtin(scene_name, device=gpu)
+    cam = rtnw.Camera.preset(cam_name, nx, ny)
+    params = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, chunk=args.chunk, seed=2024)
     out = torch.zeros(n_max, dtype=torch.float32, device=dev)
     gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     gather_list = [torch.empty(n_max, dtype=torch.float32, device=gdev) for _ in range(world)] \
@@ -168,7 +192,8 @@ def main():
             dist.gather(out if args.dist_backend == "nccl" else out.cpu(), gather_list, dst=0)
         return st
 
-    workload = f"c4: final() {nx}x{ny} pixels x {spp} spp, depth 50" + (f" over {world} GPUs" if world > 1 else "")
+    workload = f"{args.config}: {scene_name}() {nx}x{ny} pixels x {spp} spp, depth {depth}" + \
+        (f" over {world} GPUs" if world > 1 else "")
     for i in range(args.warmup):
         st = step()
         log(f"[rank {rank}] warmup {i}: kernel {st['kernel_ms']:.1f} ms")
@@ -198,7 +223,8 @@ def main():
 
     # roofline of the megakernel: algorithmic bytes (counting launch, same RNG -> same
     # paths) over the average HIP-event duration of the timed launches on this rank
-    cnt = rtnw.RenderParams(nx, ny, spp, max_depth=50, chunk=args.chunk, seed=2024, flags=rtnw.RT_FLAG_COUNT)
+    cnt = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, chunk=args.chunk, seed=2024,
+                            flags=rtnw.RT_FLAG_COUNT)
     cst = scene.render_tiles(cam, cnt, tiles, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream, stats=True)
     avg_kernel_s = float(np.mean(kms)) / 1e3
     alg = cst["algorithmic_bytes"]
@@ -216,7 +242,8 @@ def main():
 
     if rank == 0:
         res = {
-            "metric": "Msamples/s (pixels×spp/s) + achieved HBM GB/s, final() 500×500×1000spp",
+            "metric": METRIC if args.config == "c4" else
+            f"Msamples/s (pixels×spp/s) + achieved HBM GB/s, {scene_name}() {w1}×{h1}×{CONFIGS[args.config][3]}spp",
             "value": value,
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -227,13 +254,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: procedural final() scene (main.cpp:190-230), counter-RNG samples, seed 2024",
+            "data": f"synthetic: procedural {scene_name}() scene built by the host API (main.cpp builders), "
+                    f"counter-RNG samples, seed 2024",
             "config": {"workload": workload, "image": [nx, ny], "spp": spp, "pixels_per_gpu": nx * ny // world,
                        "rank_layout": ("pixel interleave %dx%d" % rtnw.interleave_factors(world)) if world > 1 else None,
                        "chunk": args.chunk,
                        "parallelism": f"pixels x{world}" + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": read_traffic(len(tiles) and sum(w * h for _, _, w, h in tiles) * spp),
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": read_traffic(nx * ny // world * spp) if args.config == "c4" else None,
                          "kernel_ms_avg": avg_kernel_s * 1e3,
                          "algorithmic_bytes_per_launch": alg,
                          "rays_per_sample": cst["segments"] / max(1.0, cst["samples"]),
@@ -244,9 +273,9 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1:
-            res["end_to_end"] = end_to_end(cam, params, nx, ny, dev)
+            res["end_to_end"] = end_to_end(scene_name, cam, params, nx, ny, dev)
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(min(16, os.cpu_count() or 1))
+            res["cpu_baseline"] = cpu_baseline(min(16, os.cpu_count() or 1), scene_name, w1, h1)
         print(json.dumps(res), flush=True)
     scene.close()
     if world > 1:
