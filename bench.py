@@ -150,7 +150,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp")
-    ap.add_argument("--chunk", type=int, default=16)
+    ap.add_argument("--chunk", type=int, default=0, help="samples per work item; 0 = the C ABI's default (1 here)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ppm", default="")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
@@ -258,7 +258,7 @@ def main():
                     f"counter-RNG samples, seed 2024",
             "config": {"workload": workload, "image": [nx, ny], "spp": spp, "pixels_per_gpu": nx * ny // world,
                        "rank_layout": ("pixel interleave %dx%d" % rtnw.interleave_factors(world)) if world > 1 else None,
-                       "chunk": args.chunk,
+                       "chunk": int(cst["chunk"]),
                        "parallelism": f"pixels x{world}" + (" + RCCL gather" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,

@@ -154,7 +154,8 @@ typedef struct rt_render_params {
     int32_t max_depth;            /* scatter while depth < max_depth (main.cpp:34: 50) */
     float t_min;                  /* main.cpp:27: 0.001 */
     int32_t background;           /* RT_BG_* */
-    int32_t chunk;                /* samples per partial sum; <= 0 selects 16 */
+    int32_t chunk;                /* samples per partial sum; <= 0 selects 1, doubled while the
+                                     slab (16 B x pixels x ceil(spp/chunk)) would pass 8 GiB */
     int32_t flags;                /* RT_FLAG_* */
     uint32_t sample_offset;       /* first sample index (progressive rendering) */
     uint32_t pad;
@@ -185,6 +186,7 @@ typedef struct rt_stats {
     double wave_prim_trips;       /*   wave-level primitive-test steps */
     double wave_sphere_draw_trips;/*   wave-level random_in_unit_sphere rejection rounds */
     double lane_sphere_draw_trips;/*   lane-level rejection rounds */
+    double chunk;                 /* samples per work item the launch used (rt_render_params.chunk or its default) */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */

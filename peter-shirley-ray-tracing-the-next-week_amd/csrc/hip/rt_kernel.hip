@@ -310,7 +310,8 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
     V3 col = mk(0, 0, 0);
-    for (int c = 0; c < nchunks; ++c) {
+#pragma unroll 8
+    for (int c = 0; c < nchunks; ++c) {   // the loads run ahead; the adds stay in chunk order
         float4 v = slab[(size_t)c * npix + p];
         col = add(col, mk(v.x, v.y, v.z));
     }

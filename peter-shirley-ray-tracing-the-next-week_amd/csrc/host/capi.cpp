@@ -77,12 +77,14 @@ rt_dprim to_dprim(const rt_prim &p, int order) {
 //   node fetch: the bytes loaded per visit (BVH2 64 B, BVH4 112 B); sphere 16 B; moving sphere 36 B;
 //   rect 24 B; instance chain entered 32 B; medium record 16 B; material +
 //   texture per shade 16 + 16 B; Perlin turbulence 7 octaves x 8 gradient gathers
-//   x (12 B gradient + 3 x 4 B permutation) = 1344 B; per work item the 16-B
-//   partial sum written and read back; 12 B of output per pixel.
-double algorithmic_bytes(const rt_stats &st, double items, double pixels, int bvh_width) {
+//   x (12 B gradient + 3 x 4 B permutation) = 1344 B; per work item the 4-B job
+//   pixel read and the 16-B partial sum written.  (rt_resolve's own traffic — the
+//   partial sums read back, the output index and the 12-B pixel — is not the
+//   megakernel's.)
+double algorithmic_bytes(const rt_stats &st, double items, int bvh_width) {
     return (bvh_width == 4 ? 112.0 : 64.0) * st.node_visits + 16.0 * st.sphere_tests + 36.0 * st.moving_sphere_tests + 24.0 * st.rect_tests +
            32.0 * st.instanced_tests + 16.0 * st.medium_tests + 32.0 * st.shades + 1344.0 * st.noise_evals +
-           32.0 * items + 12.0 * pixels;
+           20.0 * items;
 }
 
 }  // namespace
@@ -374,6 +376,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     return RT_OK;
 }
 
+// Partial-sum slab budget of the default chunk choice (bytes).
+#ifndef RT_SLAB_BUDGET
+#define RT_SLAB_BUDGET (8ull << 30)
+#endif
+
 // Job pixel order: tiles in the order given; inside a tile, bands of 8 rows listed
 // column by column (8 pixels per column), so that ANY 64 consecutive items — a wave
 // claim, wherever it starts — are 8 neighbouring columns of one band (coherent
@@ -420,7 +427,19 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     hipStream_t stream = (hipStream_t)stream_v;
     if (int rc = prepare_job(s, tiles, ntiles, p->nx, p->ny)) return rc;
 
-    const int chunk = p->chunk > 0 ? p->chunk : 16;
+    // Default chunk: one sample per work item, unless the partial-sum slab would pass
+    // RT_SLAB_BUDGET or the item count 2^32; then the smallest chunk that fits.
+    // Short items keep each wave's lanes on neighbouring pixels (a wave deals its
+    // 64-item claims to lanes as they free up; long items let its pixels drift
+    // apart): 16 -> 1 sample per item is 92.2 -> 81.8 ms on c4.
+    int chunk = p->chunk;
+    if (chunk <= 0) {
+        chunk = 1;
+        while (chunk < p->spp &&
+               ((uint64_t)s->npix * (uint64_t)((p->spp + chunk - 1) / chunk) * 16 > RT_SLAB_BUDGET ||
+                (uint64_t)s->npix * (uint64_t)((p->spp + chunk - 1) / chunk) + 64 >= 0xFFFFFFFFull))
+            chunk *= 2;
+    }
     const int nchunks = (p->spp + chunk - 1) / chunk;
     const uint64_t nitems = (uint64_t)s->npix * (uint64_t)nchunks;
     if (nitems + 64 >= 0xFFFFFFFFull) return fail(RT_ERR_INVALID, "job too large for one launch (pixels x chunks >= 2^32)");
@@ -521,6 +540,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         HIP_TRY(hipEventElapsedTime(&ms1, s->ev[1], s->ev[2]));
         std::memset(stats, 0, sizeof *stats);
         stats->samples = (double)s->npix * (double)p->spp;
+        stats->chunk = (double)chunk;
         stats->kernel_ms = ms0;
         stats->resolve_ms = ms1;
         if (count) {
@@ -536,7 +556,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->medium_tests = (double)c[RT_CNT_MEDIA];
             stats->shades = (double)c[RT_CNT_SHADES];
             stats->noise_evals = (double)c[RT_CNT_NOISE];
-            stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, (double)s->npix, s->bvh_width);
+            stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, s->bvh_width);
             unsigned long long w[5];
             HIP_TRY(hipMemcpy(w, (unsigned long long *)s->stats + RT_CNT_N + 4, sizeof w, hipMemcpyDeviceToHost));
             stats->wave_iterations = (double)w[0];

@@ -89,7 +89,7 @@ class RtStats(ctypes.Structure):
         "samples", "segments", "node_visits", "sphere_tests", "moving_sphere_tests", "rect_tests", "instanced_tests",
         "medium_tests", "shades", "noise_evals", "algorithmic_bytes", "kernel_ms", "resolve_ms",
         "cycles_claim", "cycles_traverse", "cycles_media", "cycles_shade", "grid", "wave_iterations",
-        "wave_node_trips", "wave_prim_trips", "wave_sphere_draw_trips", "lane_sphere_draw_trips")]
+        "wave_node_trips", "wave_prim_trips", "wave_sphere_draw_trips", "lane_sphere_draw_trips", "chunk")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -14,20 +14,22 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 ap = argparse.ArgumentParser()
-ap.add_argument("libs", nargs="+", help="LIB or LIB:VAR=VAL,VAR=VAL (extra environment)")
+ap.add_argument("libs", nargs="+", help="LIB or LIB:VAR=VAL,VAR=VAL (extra environment), optionally followed by "
+                                      "@ and extra bench.py arguments separated by '+' (LIB@--chunk+32)")
 ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--spp", type=int, default=1000)
 args = ap.parse_args()
 res = {lib: [] for lib in args.libs}
 for r in range(args.rounds):
     for lib in args.libs:
-        path, _, extra = lib.partition(":")
+        spec, _, bargs = lib.partition("@")
+        path, _, extra = spec.partition(":")
         env = dict(os.environ, RTNW_LIB=os.path.abspath(path))
         for kv in filter(None, extra.split(",")):
             k, _, v = kv.partition("=")
             env[k] = v
         out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                              "--spp", str(args.spp), "--no-cpu-baseline"], env=env, capture_output=True, text=True,
+                              "--spp", str(args.spp), "--no-cpu-baseline"] + list(filter(None, bargs.split("+"))), env=env, capture_output=True, text=True,
                              timeout=600)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if not line:

@@ -19,7 +19,8 @@ sc = rtnw.Scene.builtin(scene_name)
 cam = rtnw.Camera.preset(cam_name, nx, ny)
 out = {}
 for label, flags in (("plain", 0), ("profile", rtnw.RT_FLAG_PROFILE), ("count", rtnw.RT_FLAG_COUNT)):
-    p = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, flags=flags, seed=7)
+    p = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, flags=flags, seed=7,
+                          chunk=int(os.environ.get("RT_CHUNK", "0")))
     _, st = sc.render_tile(cam, p, 0, 0, nx, ny, stats=True)
     out[label] = st
 pr = out["profile"]
