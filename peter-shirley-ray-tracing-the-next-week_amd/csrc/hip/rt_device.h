@@ -550,7 +550,8 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-constexpr uint32_t kClaim = 64;   // work items claimed per wave-level atomic
+// Work items a wave claims per atomic: RtKernelArgs.claim (host: up to 512, fewer
+// for small jobs so that every wave gets work).
 
 // ------------------------------------------- cooperative rejection sampling
 // The rejection loops of the reference (camera.h:6-12 random_in_unit_disk,

@@ -38,6 +38,7 @@ struct RtKernelArgs {
     const uint32_t *job_xy;   // x | y << 16 per job pixel (image coords)
     uint32_t npix;
     uint32_t nitems;          // npix * nchunks
+    uint32_t claim;           // work items per wave-level claim (a multiple of 64)
     float4 *slab;             // [nchunks][npix] partial sums
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)

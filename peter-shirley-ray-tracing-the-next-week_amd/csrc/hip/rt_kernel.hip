@@ -14,8 +14,8 @@
 //     regenerates a new camera sample as soon as its path terminates, so lanes stay
 //     busy across bounces (path regeneration) instead of idling until the longest
 //     path of the wave finishes;
-//   * work = (chunk of `chunk` samples) x (pixel); a wave claims 64 work items per
-//     atomic (one global atomic per claim, amortised over 64 chunks) and hands them
+//   * work = (chunk of `chunk` samples) x (pixel); a wave claims A.claim (<= 512)
+//     work items per atomic (one global atomic per claim) and hands them
 //     to the lanes that need work with a ballot + mbcnt prefix count;
 //   * each item's radiance is summed in registers and stored once into a partial-sum
 //     slab [chunk][pixel]; rt_resolve sums the chunks in order (deterministic, no
@@ -124,11 +124,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         while (need_mask != 0ull && !exhausted) {
             if (pool_next == pool_end) {
                 uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(A.counter, kClaim);
+                if (lane == 0) base = atomicAdd(A.counter, A.claim);
                 base = __shfl(base, 0);
                 if (base >= A.nitems) { exhausted = true; break; }
                 pool_next = base;
-                pool_end = min(base + kClaim, A.nitems);
+                pool_end = min(base + A.claim, A.nitems);
             }
             uint32_t avail = pool_end - pool_next;
             uint32_t rank = lanes_below(need_mask);

@@ -132,11 +132,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
             while (need_mask != 0ull && !exhausted) {
                 if (pool_next == pool_end) {
                     uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(A.counter, kClaim);
+                    if (lane == 0) base = atomicAdd(A.counter, A.claim);
                     base = __shfl(base, 0);
                     if (base >= A.nitems) { exhausted = true; break; }
                     pool_next = base;
-                    pool_end = min(base + kClaim, A.nitems);
+                    pool_end = min(base + A.claim, A.nitems);
                 }
                 const uint32_t avail = pool_end - pool_next;
                 const uint32_t rank = lanes_below(need_mask);

@@ -505,6 +505,15 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     // rt_wavefront.hip)
     const char *eng = std::getenv("RTNW_ENGINE");
     const bool wave = eng && std::strcmp(eng, "wave") == 0;
+    // Claim size: up to 512 items per atomic (64 -> 512 is 81.6 -> 76.9 ms on c4: fewer
+    // round trips to the one contended counter), at least 8 claims per
+    // wave so that small jobs still spread over every wave.
+    {
+        const uint64_t waves = (uint64_t)(wave ? s->grid_wf[mode] : s->grid[mode]) * (RT_BLOCK / 64);
+        uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nitems / (waves * 8) / 64 * 64, 64), 512);
+        if (const char *e = std::getenv("RTNW_CLAIM")) c = (uint64_t)std::max(1, std::atoi(e)) * 64;   // x 64 items
+        a.claim = (uint32_t)c;
+    }
     if (wave) {
         const size_t nslots = (size_t)s->grid_wf[mode] * RT_WF_SLOTS;
         const size_t need = nslots * (5 * sizeof(float4) + sizeof(float2) + sizeof(uint4));
