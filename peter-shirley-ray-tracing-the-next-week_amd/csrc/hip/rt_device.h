@@ -531,6 +531,34 @@ __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, fl
     }
 }
 
+// One traversal round's descent (both engines).  A lane that reaches a leaf
+// postpones it (pleaf) and keeps descending speculatively until every lane holds a
+// leaf or has nothing left (Aila & Laine 2009), so node steps and leaf tests both
+// run with most lanes busy; culling against a not-yet-updated best_t is merely
+// conservative.  One branch per step (the node fetch): parking a leaf and popping
+// the stack are selects, the pop's LDS read unconditional (the exec-mask
+// bookkeeping of two more branches per step cost more: 76.2 -> 74.9 ms on c4).
+template <int kWidth, bool kCount>
+__device__ __forceinline__ uint32_t descend(const float4 *nodes, uint32_t &node, const Slab &sl, float best_t,
+                                            uint32_t *stk, int &sp, Counters &cnt) {
+    constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;   // float4 per node in HBM
+    uint32_t pleaf = RT_EMPTY_CHILD;
+    for (;;) {
+        if (!(node & RT_LEAF_BIT)) {
+            if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
+            node = node_step<kWidth>(nodes + node * kNodeStride, sl, best_t, stk, sp);
+        }
+        const bool park = node != RT_EMPTY_CHILD && (node & RT_LEAF_BIT) && pleaf == RT_EMPTY_CHILD;
+        pleaf = park ? node : pleaf;
+        node = park ? RT_EMPTY_CHILD : node;
+        const bool pop = node == RT_EMPTY_CHILD && sp > 0;
+        sp -= pop ? 1 : 0;
+        const uint32_t top = stk[(sp > 0 ? sp : 0) * 64];
+        node = pop ? top : node;
+        if (__ballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD) == 0ull) return pleaf;
+    }
+}
+
 // --------------------------------------------------------------- scatter
 // Candidates of the two rejection loops: `base` is the stream counter before the
 // candidate's first draw.

@@ -40,11 +40,6 @@ namespace {
 #define RT_READY_BATCH 48
 #endif
 
-// 1: lanes that reach a leaf keep descending until every lane holds one
-#ifndef RT_SPECULATIVE
-#define RT_SPECULATIVE 1
-#endif
-
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -56,7 +51,6 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 
 template <bool kCount, bool kProf, int kWidth>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
-    constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;   // float4 per node in HBM
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
@@ -191,27 +185,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             if (phase == PH_TRAV) {
                 // the slab test needs no exact division: boxes are padded (bvh.cpp)
                 const Slab sl = make_slab(r, A.tmin);
-                // Descend.  A lane that reaches a leaf postpones it and keeps
-                // descending speculatively until every lane holds a leaf or has
-                // nothing left (Aila & Laine 2009), so node steps and leaf tests
-                // both run with most lanes busy.  Culling against a not-yet-updated
-                // best_t is merely conservative.
-                uint32_t pleaf = RT_EMPTY_CHILD;
-                for (;;) {
-                  if (!(node & RT_LEAF_BIT)) {
-                    if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
-                    node = node_step<kWidth>(A.nodes + node * kNodeStride, sl, best_t, stk, sp);
-                  } else if (node != RT_EMPTY_CHILD && pleaf == RT_EMPTY_CHILD) {
-                    pleaf = node;   // postpone this leaf, look for the next one
-                    node = RT_EMPTY_CHILD;
-                  }
-                  if (node == RT_EMPTY_CHILD && sp > 0) {
-                    --sp;
-                    node = stk[sp * 64];
-                  }
-                  if (!RT_SPECULATIVE && pleaf != RT_EMPTY_CHILD) break;
-                  if (__ballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD) == 0ull) break;
-                }
+                const uint32_t pleaf = descend<kWidth, kCount>(A.nodes, node, sl, best_t, stk, sp, cnt);
                 if (pleaf != RT_EMPTY_CHILD) {
                     const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
                     // primitives in pairs: both 32-B heads are fetched before either test

@@ -69,7 +69,6 @@ __device__ __forceinline__ uint32_t build_list(const uint8_t *status, uint32_t w
 // list building).  Diagnostic only.
 template <bool kCount, bool kProf, int kWidth>
 __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(RtKernelArgs A) {
-    constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
@@ -236,21 +235,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 if (slot != kNone) {
                     // one round: descend (speculatively past the first leaf) until
                     // every lane holds a leaf, then test the leaves
-                    uint32_t pleaf = RT_EMPTY_CHILD;
-                    for (;;) {
-                        if (!(node & RT_LEAF_BIT)) {
-                            if (kCount) cnt.nodes++;
-                            node = node_step<kWidth>(A.nodes + node * kNodeStride, sl, best_t, stk, sp);
-                        } else if (node != RT_EMPTY_CHILD && pleaf == RT_EMPTY_CHILD) {
-                            pleaf = node;
-                            node = RT_EMPTY_CHILD;
-                        }
-                        if (node == RT_EMPTY_CHILD && sp > 0) {
-                            --sp;
-                            node = stk[sp * 64];
-                        }
-                        if (__ballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD) == 0ull) break;
-                    }
+                    const uint32_t pleaf = descend<kWidth, kCount>(A.nodes, node, sl, best_t, stk, sp, cnt);
                     if (pleaf != RT_EMPTY_CHILD) {
                         const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
                         for (uint32_t q = 0; q < nleaf; q += 2) {
