@@ -439,16 +439,23 @@ __device__ __forceinline__ Slab make_slab(const Ray &r, float tmin) {
     Slab s;
     s.ix = F2{ix, ix}; s.iy = F2{iy, iy}; s.iz = F2{iz, iz};
     s.nox = F2{-r.o.x * ix, -r.o.x * ix}; s.noy = F2{-r.o.y * iy, -r.o.y * iy}; s.noz = F2{-r.o.z * iz, -r.o.z * iz};
-    s.tmin = __builtin_canonicalizef(tmin);   // known canonical: no re-quieting per use
+    s.tmin = tmin;
     return s;
 }
 // entry distance of one child box, +inf if the ray misses it (or, kSlots, the slot
 // is empty: BVH4 nodes may have unused slots; BVH2 interior nodes never do)
 // [tn, tf] of one child box (a hit iff tn <= tf; NaN slabs are ignored by min/max)
+// The clamps to [tmin, best_t] are signed-integer max/min on the float bits: exact
+// when either operand is >= 0, and when both are negative they pick the value
+// further out (tn lower, tf higher), i.e. conservative; a NaN from all three axes
+// (zero direction) culls the box, where the primitives could not be hit either.
+// Float min/max would need tmin and best_t canonicalised in every step (3 VALU).
+__device__ __forceinline__ float imax(float a, float b) { return __int_as_float(max(__float_as_int(a), __float_as_int(b))); }
+__device__ __forceinline__ float imin(float a, float b) { return __int_as_float(min(__float_as_int(a), __float_as_int(b))); }
 __device__ __forceinline__ void box_span(const Slab &s, F2 x, F2 y, F2 z, float best_t, float &tn, float &tf) {
     const F2 a = pk_fma(x, s.ix, s.nox), b = pk_fma(y, s.iy, s.noy), e = pk_fma(z, s.iz, s.noz);
-    tn = vmax3(vmin(a.x, a.y), vmin(b.x, b.y), vmax(vmin(e.x, e.y), s.tmin));
-    tf = vmin3(vmax(a.x, a.y), vmax(b.x, b.y), vmin(vmax(e.x, e.y), best_t));
+    tn = imax(vmax3(vmin(a.x, a.y), vmin(b.x, b.y), vmin(e.x, e.y)), s.tmin);
+    tf = imin(vmin3(vmax(a.x, a.y), vmax(b.x, b.y), vmax(e.x, e.y)), best_t);
 }
 template <bool kSlots>
 __device__ __forceinline__ float box_entry(const Slab &s, F2 x, F2 y, F2 z, float best_t, uint32_t c) {
