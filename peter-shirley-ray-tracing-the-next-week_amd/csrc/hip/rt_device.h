@@ -475,15 +475,11 @@ __device__ __forceinline__ void cas(float &ka, uint32_t &ca, float &kb, uint32_t
 // One interior node: test the children, push the hit ones but the nearest far to
 // near (branch-free: a slot is written, then kept only if the child was hit; the
 // builder bounds sp by RT_STACK_DEPTH - 1), return the nearest (or empty).
-#ifndef RT_NODE_MASKS
-#define RT_NODE_MASKS 0
-#endif
 template <int kWidth>
 __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, float best_t, uint32_t *stk, int &sp) {
     if (kWidth == 2) {   // rt_dnode2
         const float4 b0 = N[0], b1 = N[1], b2 = N[2], cf = N[3];
         const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-#if RT_NODE_MASKS == 0
         const float k0 = box_entry<false>(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, c0);
         const float k1 = box_entry<false>(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, c1);
         const bool second = k1 < k0;   // ties: child 0 first
@@ -492,29 +488,6 @@ __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, fl
         stk[sp * 64] = farc;
         sp += kf != RT_INF;
         return kn != RT_INF ? nearc : RT_EMPTY_CHILD;
-#else
-        // the two hit tests and the entry order are independent compares, combined
-        // as lane masks (no select-then-compare chain): the order is that of
-        // k = hit ? tn : inf with ties to child 0, since a hit child's tn is finite
-        float tn0, tf0, tn1, tf1;
-        box_span(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, tn0, tf0);
-        box_span(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, tn1, tf1);
-        const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
-#if RT_NODE_MASKS == 1
-        const bool second = h1 && (tn1 < tn0 || !h0);
-        const uint32_t nearc = second ? c1 : c0, farc = second ? c0 : c1;
-        stk[sp * 64] = farc;
-        sp += h0 && h1;
-        return (h0 || h1) ? nearc : RT_EMPTY_CHILD;
-#else
-        const bool lt = tn1 < tn0;
-        const bool second = h1 & (lt | !h0);
-        const uint32_t nearc = second ? c1 : c0, farc = second ? c0 : c1;
-        stk[sp * 64] = farc;
-        sp += h0 & h1;
-        return (h0 | h1) ? nearc : RT_EMPTY_CHILD;
-#endif
-#endif
     } else {             // rt_dnode4
         const float4 qx01 = N[0], qx23 = N[1], qy01 = N[2], qy23 = N[3], qz01 = N[4], qz23 = N[5], cf = N[6];
         uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y), c2 = (uint32_t)fbits(cf.z),
