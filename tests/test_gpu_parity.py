@@ -218,6 +218,31 @@ def test_full_resolution_sampled_crops(scene, nx, ny):
         assert (gamma_rms(g[y0:y0 + 8, x0:x0 + 8], o) <= TOL_RMS).all()
 
 
+def test_default_work_item_is_one_sample_in_reference_order():
+    """chunk <= 0 selects one sample per work item (capi.cpp): the resolve then adds
+    the samples one at a time, the reference's `col += temp` order (main.cpp:311), so
+    the image equals the single-partial-sum render (chunk = spp) bit for bit."""
+    nx, ny, ns = 40, 24, 12
+    cam = rtnw.Camera.preset("cornell", nx, ny)
+    sc = _scene("final")
+    a, st = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=6), 0, 0, nx, ny, stats=True)
+    b = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=6, chunk=ns), 0, 0, nx, ny)
+    assert st["chunk"] == 1
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    o = oracle_render("final", nx, ny, ns, seed=6, chunk=1)
+    assert (gamma_rms(a, o) <= TOL_RMS).all()
+
+
+@pytest.mark.parametrize("claim", ["1", "3", "16"])
+def test_claim_size_does_not_change_the_image(monkeypatch, claim):
+    """Work items per wave-level claim (RTNW_CLAIM x 64) only change which lane runs
+    which sample: the partial-sum slot of a sample is fixed, so images agree bitwise."""
+    ref = gpu_render("final", 64, 40, 8, seed=8, chunk=1)
+    monkeypatch.setenv("RTNW_CLAIM", claim)
+    img = gpu_render("final", 64, 40, 8, seed=8, chunk=1)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+
+
 def test_medium_size_final_parity():
     g = gpu_render("final", 100, 100, 32, seed=13)
     o = oracle_render("final", 100, 100, 32, seed=13)
