@@ -229,14 +229,17 @@ __device__ __forceinline__ int rect_axis(int kind) { return 4 - kind; }
 // for a rect (aarect.h:51) — is ONE IEEE division either way.  Every value is the
 // same float the per-kind code computes (same operands, same operations); only
 // the moving-sphere centre and a sphere's second root stay behind branches.
+// kInst = false: the scene has no instance chains (the host knows), so the kernel
+// carries no instance code at all (fewer registers live across the leaf tests).
+template <bool kInst = true>
 __device__ __forceinline__ float prim_t_head(float4 g0, float4 mm, const float4 *P, const float4 *insts, uint32_t idx,
                                              const Ray &r0, float tmin, int &key, int &kind_out) {
     const int kind = fbits(mm.x) & 0xff;
     const int inst = fbits(mm.z);
     const int order = fbits(mm.w);
-    kind_out = kind | (inst >= 0 ? 0x100 : 0);
+    kind_out = kind | (kInst && inst >= 0 ? 0x100 : 0);
     Ray r = r0;
-    if (inst >= 0) r = to_object(insts, inst, r0);
+    if (kInst && inst >= 0) r = to_object(insts, inst, r0);
     const bool sph = kind <= RT_PRIM_MOVING_SPHERE;
     key = sph ? order : -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
     // sphere.h:25-52 (moving: the centre at r.time, sphere.h:81-83)
@@ -265,9 +268,10 @@ __device__ __forceinline__ float prim_t_head(float4 g0, float4 mm, const float4 
     return (ai < g0.x || ai > g0.y || bj < g0.z || bj > g0.w) ? RT_INF : t;
 }
 
+template <bool kInst = true>
 __device__ __forceinline__ float prim_t(const float4 *P, const float4 *insts, uint32_t idx, const Ray &r0, float tmin,
                                         int &key, int &kind_out) {
-    return prim_t_head(P[idx * 4 + 0], P[idx * 4 + 1], P, insts, idx, r0, tmin, key, kind_out);
+    return prim_t_head<kInst>(P[idx * 4 + 0], P[idx * 4 + 1], P, insts, idx, r0, tmin, key, kind_out);
 }
 
 struct Hit { V3 p, n; float u, v; int mat; };
@@ -284,6 +288,7 @@ __device__ __forceinline__ void sphere_uv(V3 p, float &u, float &v) {
 // 103-106; aarect.h:58-63; hitable.h:43-45, 69, 137-145).
 // (u, v) is computed only for materials whose texture reads it (an image texture):
 // every other texture ignores it (texture.h:22-56).
+template <bool kInst = true>
 __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts, const float4 *mats, uint32_t idx,
                                            const Ray &r0, float t) {
     const float4 g0 = P[idx * 4 + 0];
@@ -292,7 +297,7 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
     int flip = (fbits(mm.x) >> 8) & 1;
     int inst = fbits(mm.z);
     Ray r = r0;
-    if (inst >= 0) r = to_object(insts, inst, r0);
+    if (kInst && inst >= 0) r = to_object(insts, inst, r0);
     Hit h;
     h.p = at(r, t);
     if (kind == RT_PRIM_SPHERE) {
@@ -320,7 +325,7 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
         }
     }
     if (flip) h.n = neg(h.n);
-    if (inst >= 0) to_world(insts, inst, h.p, h.n);
+    if (kInst && inst >= 0) to_world(insts, inst, h.p, h.n);
     return h;
 }
 
@@ -343,13 +348,13 @@ struct Counters {
     }
 };
 
-template <bool kCount>
+template <bool kCount, bool kInst = true>
 __device__ __forceinline__ float boundary_t(const float4 *B, const float4 *insts, int first, int count, const Ray &r,
                                             float tmin, Counters &cnt) {
     float best = RT_INF;
     for (int q = 0; q < count; ++q) {
         int key, kind;
-        float t = prim_t(B, insts, (uint32_t)(first + q), r, tmin, key, kind);
+        float t = prim_t<kInst>(B, insts, (uint32_t)(first + q), r, tmin, key, kind);
         if (kCount) cnt.prim(kind);
         if (t < best) best = t;
     }
@@ -749,7 +754,7 @@ __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds
 }
 
 // One medium's test (constant_medium.h:26-50) against the surface result.
-template <bool kCount>
+template <bool kCount, bool kInst = true>
 __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, int depth,
                                            const Rng &g, bool &have, float &best_t, int &med_mat, Counters &cnt) {
     if (kCount) cnt.media++;
@@ -779,10 +784,10 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
         r2 = ga ? ta : tb;
         ok = valid && (fa || fb) && (ga || gb);
     } else {
-        r1 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
+        r1 = boundary_t<kCount, kInst>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
         ok = r1 != RT_INF;
         if (__ballot(ok) == 0ull) return;
-        r2 = boundary_t<kCount>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
+        r2 = boundary_t<kCount, kInst>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
         ok = ok && r2 != RT_INF;
     }
     const float tmax = have ? best_t : RT_FLT_MAX;
@@ -806,7 +811,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
 // copy through an explicit LDS pointer, the rest from HBM, in two loops: one loop
 // choosing per medium between the two made the compiler select the address and
 // issue generic (flat) loads, which wait on both memory counters.
-template <bool kCount>
+template <bool kCount, bool kInst = true>
 __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, int depth,
                                          const Rng &g, bool &have, float &best_t, Counters &cnt) {
     typedef unsigned U4v __attribute__((ext_vector_type(4)));
@@ -820,14 +825,14 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
         M.md = make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
         M.g0 = make_float4(__uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w));
         M.mm = make_float4(__uint_as_float(z.x), __uint_as_float(z.y), __uint_as_float(z.z), __uint_as_float(z.w));
-        medium_one<kCount>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
     }
     for (int k = RT_LDS_MEDIA; k < A.nmedia; ++k) {
         MediumRec M;
         M.md = A.media[k];
         M.g0 = A.bprims[M.md.x * 4 + 0];
         M.mm = A.bprims[M.md.x * 4 + 1];
-        medium_one<kCount>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
     }
     return med_mat;
 }

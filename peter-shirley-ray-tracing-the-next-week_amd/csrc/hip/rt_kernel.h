@@ -24,6 +24,7 @@ struct RtKernelArgs {
     int bvh_width;          // 2 or 4
     int has_bvh;
     int nmedia;
+    int has_instances;      // any instance chain (selects the megakernel variant)
     // camera (camera.h members)
     float org[3], llc[3], hor[3], ver[3], cu[3], cv[3];
     float lens, ct0, ct1;

@@ -49,7 +49,9 @@ namespace {
 // Lane phases of the batched state machine below.
 enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 
-template <bool kCount, bool kProf, int kWidth>
+// kInst: the scene has translate / rotate_y / flip_normals chains (cornell scenes);
+// final() and the random scenes run the variant without instance code.
+template <bool kCount, bool kProf, int kWidth, bool kInst>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
@@ -196,13 +198,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                         const float4 ga = A.prims[ia * 4 + 0], ma = A.prims[ia * 4 + 1];
                         const float4 gb = A.prims[ib * 4 + 0], mb = A.prims[ib * 4 + 1];
                         int key, kind;
-                        float t = prim_t_head(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
+                        float t = prim_t_head<kInst>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
                         if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
                         if (t < best_t || (t == best_t && key < best_key)) {
                             best_t = t; best_key = key; best_prim = ia;
                         }
                         if (two) {
-                            t = prim_t_head(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
+                            t = prim_t_head<kInst>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
                             if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
                             if (t < best_t || (t == best_t && key < best_key)) {
                                 best_t = t; best_key = key; best_prim = ib;
@@ -224,13 +226,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            const int med_mat = media_hit<kCount>(A, lds_media, r, depth, g, have, best_t, cnt);
+            const int med_mat = media_hit<kCount, kInst>(A, lds_media, r, depth, g, have, best_t, cnt);
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);
                 hr.mat = med_mat;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
             } else if (have) {
-                hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
+                hr = prim_record<kInst>(A.prims, A.insts, A.mats, best_prim, r, best_t);
             }
         }
 
@@ -298,19 +300,21 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
 }  // namespace
 
 // --------------------------------------------------------------- launchers
-template <int kWidth>
-static hipError_t launch_width(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
+template <int kWidth, bool kInst>
+static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (mode == 1)
-        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth, kInst>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else if (mode == 2)
-        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth, kInst>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else
-        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth, kInst>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     return hipGetLastError();
 }
 
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
-    return a->bvh_width == 4 ? launch_width<4>(a, grid, mode, stream) : launch_width<2>(a, grid, mode, stream);
+    if (a->bvh_width == 4)
+        return a->has_instances ? launch_variant<4, true>(a, grid, mode, stream) : launch_variant<4, false>(a, grid, mode, stream);
+    return a->has_instances ? launch_variant<2, true>(a, grid, mode, stream) : launch_variant<2, false>(a, grid, mode, stream);
 }
 
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, const uint32_t *out_index,
@@ -323,10 +327,10 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
 template <int kWidth>
 static hipError_t occupancy_width(int *blocks_per_cu, int mode) {
     if (mode == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, true>, RT_BLOCK, 0);
     if (mode == 2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, true>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, true>, RT_BLOCK, 0);
 }
 
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width) {

@@ -99,7 +99,7 @@ struct rt_scene {
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
          *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr;
     uint32_t root = 0;
-    int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2;
+    int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
     bool has_moving = false;
     float time0 = 0, time1 = 1;
     // job cache
@@ -349,6 +349,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->nnodes = (int)(bvh.width == 4 ? bvh.nodes4.size() : bvh.nodes2.size());
     s->bvh_width = bvh.width;
     s->nprims = d->nprims;
+    s->ninstances = d->ninstances;
 
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return cleanup(hip_fail(e, "hipGetDeviceProperties"));
@@ -473,6 +474,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.bvh_width = s->bvh_width;
     a.has_bvh = s->has_bvh;
     a.nmedia = s->nmedia;
+    a.has_instances = s->ninstances > 0;
     for (int k = 0; k < 3; k++) {
         a.org[k] = cam->origin[k];
         a.llc[k] = cam->lower_left_corner[k];
