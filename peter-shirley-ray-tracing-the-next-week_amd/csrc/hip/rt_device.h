@@ -288,7 +288,9 @@ __device__ __forceinline__ void sphere_uv(V3 p, float &u, float &v) {
 // 103-106; aarect.h:58-63; hitable.h:43-45, 69, 137-145).
 // (u, v) is computed only for materials whose texture reads it (an image texture):
 // every other texture ignores it (texture.h:22-56).
-template <bool kInst = true>
+// kUV = false: no material of the scene reads (u, v) (no image texture), so the
+// uv code (sphere: atan2/asin + double divisions) is not compiled in.
+template <bool kInst = true, bool kUV = true>
 __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts, const float4 *mats, uint32_t idx,
                                            const Ray &r0, float t) {
     const float4 g0 = P[idx * 4 + 0];
@@ -311,7 +313,7 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
     h.u = 0.f;
     h.v = 0.f;
     h.mat = fbits(mm.x) >> 9;
-    if (fbits(mats[h.mat * 2 + 1].w) & 1) {
+    if (kUV && (fbits(mats[h.mat * 2 + 1].w) & 1)) {
         if (kind == RT_PRIM_SPHERE) {
             sphere_uv(divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w), h.u, h.v);   // sphere.h:36
         } else if (kind != RT_PRIM_MOVING_SPHERE) {                          // aarect.h:54-59
@@ -416,9 +418,10 @@ __device__ __forceinline__ int tex_leaf(const RtKernelArgs &A, int ti, V3 p, flo
 
 // texture::value of a constant or image leaf (texture.h:16-27; surface_texture.h:19-30);
 // the noise leaf is finished after coop_turb.
+template <bool kUV = true>
 __device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, float4 t0, float4 t1, float u, float v) {
     if (kind == RT_TEX_CONSTANT) return mk(t1.x, t1.y, t1.z);
-    if (kind == RT_TEX_IMAGE) {   // stride 3 as the reference addresses it
+    if (kUV && kind == RT_TEX_IMAGE) {   // stride 3 as the reference addresses it
         const int nx = fbits(t0.y), ny = fbits(t0.z);
         const uint8_t *data = A.texels + fbits(t0.w);
         int i = (int)((1 - u) * nx);
@@ -850,7 +853,7 @@ struct ShadeOut {
     V3 att, emitted;
     Ray ray;
 };
-template <bool kCount>
+template <bool kCount, bool kUV = true>
 __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, bool have, const Ray &r, const Hit &hr,
                                           int depth, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt) {
     const bool shading = ready && have;
@@ -869,7 +872,7 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
             const int tkind = tex_leaf(A, fbits(A.mats[hr.mat * 2 + 0].y), hr.p, t0, t1);   // texture.h:35-44
             noisy = tkind == RT_TEX_NOISE;
             nscale = t0.w;
-            if (!noisy) tv = tex_value_leaf(A, tkind, t0, t1, hr.u, hr.v);
+            if (!noisy) tv = tex_value_leaf<kUV>(A, tkind, t0, t1, hr.u, hr.v);
         }
     }
     if (kCount && noisy) cnt.noise++;

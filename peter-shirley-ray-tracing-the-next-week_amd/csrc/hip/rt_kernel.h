@@ -24,7 +24,8 @@ struct RtKernelArgs {
     int bvh_width;          // 2 or 4
     int has_bvh;
     int nmedia;
-    int has_instances;      // any instance chain (selects the megakernel variant)
+    int has_instances;      // any instance chain     } select the megakernel variant
+    int has_uv;             // any material reads u,v }
     // camera (camera.h members)
     float org[3], llc[3], hor[3], ver[3], cu[3], cv[3];
     float lens, ct0, ct1;

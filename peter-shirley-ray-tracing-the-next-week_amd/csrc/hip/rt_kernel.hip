@@ -50,8 +50,9 @@ namespace {
 enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 
 // kInst: the scene has translate / rotate_y / flip_normals chains (cornell scenes);
-// final() and the random scenes run the variant without instance code.
-template <bool kCount, bool kProf, int kWidth, bool kInst>
+// kUV: a material reads (u, v) (image textures: earth()).  final() and the random
+// scenes run the variant with neither.
+template <bool kCount, bool kProf, int kWidth, bool kInst, bool kUV>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
@@ -232,13 +233,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
                 hr.n = mk(1, 0, 0);
                 hr.mat = med_mat;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
             } else if (have) {
-                hr = prim_record<kInst>(A.prims, A.insts, A.mats, best_prim, r, best_t);
+                hr = prim_record<kInst, kUV>(A.prims, A.insts, A.mats, best_prim, r, best_t);
             }
         }
 
         mark(2);
         // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
-        const ShadeOut so = shade<kCount>(A, ready, have, r, hr, depth, g, slots, lane, cnt);
+        const ShadeOut so = shade<kCount, kUV>(A, ready, have, r, hr, depth, g, slots, lane, cnt);
         if (ready) {
             if (so.scattered) {
                 beta = mul(beta, so.att);
@@ -300,21 +301,28 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
 }  // namespace
 
 // --------------------------------------------------------------- launchers
-template <int kWidth, bool kInst>
+template <int kWidth, bool kInst, bool kUV>
 static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (mode == 1)
-        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth, kInst>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth, kInst, kUV>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else if (mode == 2)
-        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth, kInst>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth, kInst, kUV>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else
-        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth, kInst>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth, kInst, kUV>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     return hipGetLastError();
 }
 
+template <int kWidth>
+static hipError_t launch_width(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
+    if (a->has_instances)
+        return a->has_uv ? launch_variant<kWidth, true, true>(a, grid, mode, stream)
+                         : launch_variant<kWidth, true, false>(a, grid, mode, stream);
+    return a->has_uv ? launch_variant<kWidth, false, true>(a, grid, mode, stream)
+                     : launch_variant<kWidth, false, false>(a, grid, mode, stream);
+}
+
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
-    if (a->bvh_width == 4)
-        return a->has_instances ? launch_variant<4, true>(a, grid, mode, stream) : launch_variant<4, false>(a, grid, mode, stream);
-    return a->has_instances ? launch_variant<2, true>(a, grid, mode, stream) : launch_variant<2, false>(a, grid, mode, stream);
+    return a->bvh_width == 4 ? launch_width<4>(a, grid, mode, stream) : launch_width<2>(a, grid, mode, stream);
 }
 
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, const uint32_t *out_index,
@@ -327,10 +335,10 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
 template <int kWidth>
 static hipError_t occupancy_width(int *blocks_per_cu, int mode) {
     if (mode == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, true>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, true, true>, RT_BLOCK, 0);
     if (mode == 2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, true>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, true>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, true, true>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, true, true>, RT_BLOCK, 0);
 }
 
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width) {

@@ -101,6 +101,7 @@ struct rt_scene {
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
     bool has_moving = false;
+    bool has_uv = false;     // a material reads (u, v)
     float time0 = 0, time1 = 1;
     // job cache
     std::vector<int32_t> job_tiles;
@@ -296,6 +297,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             o.albedo[2] = m.ref_idx * m.ref_idx;              // ref_idx^2 of the exit cosine
         }
         o.flags = (m.texture >= 0 && reads_uv(m.texture)) ? 1 : 0;
+        s->has_uv |= o.flags != 0;
     }
     std::vector<rt_dtexture> texs(d->ntextures);
     for (int i = 0; i < d->ntextures; i++) {
@@ -475,6 +477,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.has_bvh = s->has_bvh;
     a.nmedia = s->nmedia;
     a.has_instances = s->ninstances > 0;
+    a.has_uv = s->has_uv;
     for (int k = 0; k < 3; k++) {
         a.org[k] = cam->origin[k];
         a.llc[k] = cam->lower_left_corner[k];
