@@ -404,7 +404,14 @@ __device__ __forceinline__ float perlin_noise(const float4 *ranvec, const int *p
 
 // Texture chain of one lane down to its leaf: checker_texture picks a child by
 // the sign of the sines (texture.h:35-44).  Returns the leaf kind (-1: chain too deep).
+// kChecker = false: the scene has no checker_texture, the leaf is the material's own.
+template <bool kChecker = true>
 __device__ __forceinline__ int tex_leaf(const RtKernelArgs &A, int ti, V3 p, float4 &t0, float4 &t1) {
+    if (!kChecker) {
+        t0 = A.texs[ti * 2 + 0];
+        t1 = A.texs[ti * 2 + 1];
+        return fbits(t0.x);
+    }
     for (int guard = 0; guard < RT_MAX_CHECKER_DEPTH; ++guard) {
         t0 = A.texs[ti * 2 + 0];
         t1 = A.texs[ti * 2 + 1];
@@ -853,7 +860,7 @@ struct ShadeOut {
     V3 att, emitted;
     Ray ray;
 };
-template <bool kCount, bool kUV = true>
+template <bool kCount, bool kUV = true, bool kChecker = true>
 __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, bool have, const Ray &r, const Hit &hr,
                                           int depth, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt) {
     const bool shading = ready && have;
@@ -869,7 +876,7 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
                               (live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC));
         if (textured) {
             float4 t0, t1;
-            const int tkind = tex_leaf(A, fbits(A.mats[hr.mat * 2 + 0].y), hr.p, t0, t1);   // texture.h:35-44
+            const int tkind = tex_leaf<kChecker>(A, fbits(A.mats[hr.mat * 2 + 0].y), hr.p, t0, t1);   // texture.h:35-44
             noisy = tkind == RT_TEX_NOISE;
             nscale = t0.w;
             if (!noisy) tv = tex_value_leaf<kUV>(A, tkind, t0, t1, hr.u, hr.v);

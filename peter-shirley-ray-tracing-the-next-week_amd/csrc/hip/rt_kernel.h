@@ -7,6 +7,12 @@
 #define RT_BLOCK 256      // 4 waves per workgroup
 #define RT_WF_SLOTS 1024  // path slots per workgroup of the wavefront engine
 
+// scene features a megakernel variant carries code for (rt_launch_megakernel)
+#define RT_FEAT_INST 1      // translate / rotate_y / flip_normals chains
+#define RT_FEAT_UV 2        // a material reads (u, v): image_texture
+#define RT_FEAT_CHECKER 4   // checker_texture
+#define RT_FEAT_ALL 7
+
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)
     const float4 *nodes;    // BVH nodes, breadth-first: 4 x float4 (width 2) or 8 x float4 (width 4)
@@ -24,8 +30,7 @@ struct RtKernelArgs {
     int bvh_width;          // 2 or 4
     int has_bvh;
     int nmedia;
-    int has_instances;      // any instance chain     } select the megakernel variant
-    int has_uv;             // any material reads u,v }
+    int features;           // RT_FEAT_* present in the scene (selects the megakernel variant)
     // camera (camera.h members)
     float org[3], llc[3], hor[3], ver[3], cu[3], cv[3];
     float lens, ct0, ct1;

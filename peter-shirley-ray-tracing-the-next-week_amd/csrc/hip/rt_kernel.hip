@@ -49,11 +49,14 @@ namespace {
 // Lane phases of the batched state machine below.
 enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 
-// kInst: the scene has translate / rotate_y / flip_normals chains (cornell scenes);
-// kUV: a material reads (u, v) (image textures: earth()).  final() and the random
-// scenes run the variant with neither.
-template <bool kCount, bool kProf, int kWidth, bool kInst, bool kUV>
+// kFeat (RT_FEAT_*): the scene features the variant carries code for — instance
+// chains (cornell scenes), (u, v)-reading materials (earth()), checker textures
+// (the random scenes).  The host launches the smallest compiled variant covering
+// the scene (final(): none of them); RT_FEAT_ALL runs anything.
+template <bool kCount, bool kProf, int kWidth, int kFeat>
 __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
+    constexpr bool kInst = (kFeat & RT_FEAT_INST) != 0, kUV = (kFeat & RT_FEAT_UV) != 0,
+                   kChecker = (kFeat & RT_FEAT_CHECKER) != 0;
     __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
     __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
 
         mark(2);
         // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
-        const ShadeOut so = shade<kCount, kUV>(A, ready, have, r, hr, depth, g, slots, lane, cnt);
+        const ShadeOut so = shade<kCount, kUV, kChecker>(A, ready, have, r, hr, depth, g, slots, lane, cnt);
         if (ready) {
             if (so.scattered) {
                 beta = mul(beta, so.att);
@@ -301,28 +304,28 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
 }  // namespace
 
 // --------------------------------------------------------------- launchers
-template <int kWidth, bool kInst, bool kUV>
+template <int kWidth, int kFeat>
 static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (mode == 1)
-        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth, kInst, kUV>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth, kFeat>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else if (mode == 2)
-        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth, kInst, kUV>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth, kFeat>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     else
-        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth, kInst, kUV>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth, kFeat>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
     return hipGetLastError();
 }
 
-template <int kWidth>
-static hipError_t launch_width(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
-    if (a->has_instances)
-        return a->has_uv ? launch_variant<kWidth, true, true>(a, grid, mode, stream)
-                         : launch_variant<kWidth, true, false>(a, grid, mode, stream);
-    return a->has_uv ? launch_variant<kWidth, false, true>(a, grid, mode, stream)
-                     : launch_variant<kWidth, false, false>(a, grid, mode, stream);
-}
-
+// Compiled variants: every feature (any scene), none (final()), instances only
+// (cornell_box, cornell_smoke), checker only (the random scenes); BVH4 always runs
+// the all-feature variant.
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
-    return a->bvh_width == 4 ? launch_width<4>(a, grid, mode, stream) : launch_width<2>(a, grid, mode, stream);
+    if (a->bvh_width == 4) return launch_variant<4, RT_FEAT_ALL>(a, grid, mode, stream);
+    switch (a->features) {
+    case 0: return launch_variant<2, 0>(a, grid, mode, stream);
+    case RT_FEAT_INST: return launch_variant<2, RT_FEAT_INST>(a, grid, mode, stream);
+    case RT_FEAT_CHECKER: return launch_variant<2, RT_FEAT_CHECKER>(a, grid, mode, stream);
+    default: return launch_variant<2, RT_FEAT_ALL>(a, grid, mode, stream);
+    }
 }
 
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, const uint32_t *out_index,
@@ -335,10 +338,10 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
 template <int kWidth>
 static hipError_t occupancy_width(int *blocks_per_cu, int mode) {
     if (mode == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, true, true>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, RT_FEAT_ALL>, RT_BLOCK, 0);
     if (mode == 2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, true, true>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, true, true>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, RT_FEAT_ALL>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, RT_FEAT_ALL>, RT_BLOCK, 0);
 }
 
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width) {

@@ -101,7 +101,8 @@ struct rt_scene {
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
     bool has_moving = false;
-    bool has_uv = false;     // a material reads (u, v)
+    bool has_uv = false;       // a material reads (u, v)
+    bool has_checker = false;  // a checker_texture exists
     float time0 = 0, time1 = 1;
     // job cache
     std::vector<int32_t> job_tiles;
@@ -306,6 +307,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         o.kind = t.kind;
         o.even = t.even;
         o.odd = t.odd;
+        s->has_checker |= t.kind == RT_TEX_CHECKER;
         o.scale = t.scale;
         for (int k = 0; k < 3; k++) o.color[k] = t.color[k];
         if (t.kind == RT_TEX_IMAGE) {   // (kind, nx, ny, byte offset)
@@ -476,8 +478,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.bvh_width = s->bvh_width;
     a.has_bvh = s->has_bvh;
     a.nmedia = s->nmedia;
-    a.has_instances = s->ninstances > 0;
-    a.has_uv = s->has_uv;
+    a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
+                 (s->has_checker ? RT_FEAT_CHECKER : 0);
     for (int k = 0; k < 3; k++) {
         a.org[k] = cam->origin[k];
         a.llc[k] = cam->lower_left_corner[k];
