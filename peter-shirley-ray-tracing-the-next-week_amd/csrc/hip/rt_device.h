@@ -765,7 +765,7 @@ __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds
 
 // One medium's test (constant_medium.h:26-50) against the surface result.
 template <bool kCount, bool kInst = true>
-__device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, int depth,
+__device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, float dlen, int depth,
                                            const Rng &g, bool &have, float &best_t, int &med_mat, Counters &cnt) {
     if (kCount) cnt.media++;
     const int4 md = M.md;
@@ -806,7 +806,6 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     ok = ok && !(r1 >= r2);
     if (__ballot(ok) == 0ull) return;   // no lane inside the medium: no free-flight draw
     r1 = r1 < 0 ? 0.f : r1;
-    const float dlen = len(r.d);
     const float distance_inside_boundary = (r2 - r1) * dlen;
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
     const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k)));
@@ -822,7 +821,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
 // choosing per medium between the two made the compiler select the address and
 // issue generic (flat) loads, which wait on both memory counters.
 template <bool kCount, bool kInst = true>
-__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, int depth,
+__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, float dlen, int depth,
                                          const Rng &g, bool &have, float &best_t, Counters &cnt) {
     typedef unsigned U4v __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) const U4v LdsU4;
@@ -835,14 +834,14 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
         M.md = make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
         M.g0 = make_float4(__uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w));
         M.mm = make_float4(__uint_as_float(z.x), __uint_as_float(z.y), __uint_as_float(z.z), __uint_as_float(z.w));
-        medium_one<kCount, kInst>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, dlen, depth, g, have, best_t, med_mat, cnt);
     }
     for (int k = RT_LDS_MEDIA; k < A.nmedia; ++k) {
         MediumRec M;
         M.md = A.media[k];
         M.g0 = A.bprims[M.md.x * 4 + 0];
         M.mm = A.bprims[M.md.x * 4 + 1];
-        medium_one<kCount, kInst>(A, M, k, r, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, dlen, depth, g, have, best_t, med_mat, cnt);
     }
     return med_mat;
 }
@@ -861,8 +860,10 @@ struct ShadeOut {
     Ray ray;
 };
 template <bool kCount, bool kUV = true, bool kChecker = true>
-__device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, bool have, const Ray &r, const Hit &hr,
-                                          int depth, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt) {
+// dlen = |r.d|, computed once per segment and shared with the media (RtKernelArgs.need_dlen).
+__device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, bool have, const Ray &r, float dlen,
+                                          const Hit &hr, int depth, Rng &g, CoopSlot *slots, uint32_t lane,
+                                          Counters &cnt) {
     const bool shading = ready && have;
     int kind = -1;
     bool live = false, noisy = false;
@@ -897,10 +898,15 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
     o.att = mk(0, 0, 0);
     o.emitted = mk(0, 0, 0);
     o.ray = r;
+    // unit(r.d) (vec3.h:146) once, for the lanes whose shading needs it — metal,
+    // dielectric, the sky — instead of once in each of their branches
+    const bool wants_unit = ready && (have ? live && (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC)
+                                           : A.background == RT_BG_SKY);
+    V3 ud = mk(0, 0, 0);
+    if (wants_unit) ud = divs(r.d, dlen);
     if (!ready) return o;
     if (!have) {
         if (A.background == RT_BG_SKY) {                                  // TNW/Chapter03:29-31
-            V3 ud = unit(r.d);
             float t = (float)(0.5 * ((double)ud.y + 1.0));
             o.emitted = add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
         }
@@ -917,7 +923,7 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
         o.att = tv;
         o.scattered = true;
     } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
-        V3 reflected = reflect(unit(r.d), hr.n);
+        V3 reflected = reflect(ud, hr.n);
         ns.o = hr.p; ns.d = add(reflected, scale(m0.z, rius)); ns.time = 0.0f;
         o.att = mk(m1.x, m1.y, m1.z);
         o.scattered = dot(ns.d, hr.n) > 0;
@@ -931,15 +937,15 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
         if (dn > 0) {
             outward_normal = neg(hr.n);
             ni_over_nt = ref_idx;
-            cosine = dot(r.d, hr.n) / len(r.d);
+            cosine = dot(r.d, hr.n) / dlen;
             cosine = sqrtf(1 - m1.z * (1 - cosine * cosine));   // m1.z = ref_idx * ref_idx
         } else {
             outward_normal = hr.n;
             ni_over_nt = m1.x;                                   // (float)(1.0 / (double)ref_idx)
-            cosine = -dot(r.d, hr.n) / len(r.d);
+            cosine = -dot(r.d, hr.n) / dlen;
         }
         // refract, material.h:23-33
-        V3 uv = unit(r.d);
+        const V3 uv = ud;
         float dt = dot(uv, outward_normal);
         float disc = (float)(1.0 - (double)(ni_over_nt * ni_over_nt * (1 - dt * dt)));
         float reflect_prob;

@@ -31,6 +31,7 @@ struct RtKernelArgs {
     int has_bvh;
     int nmedia;
     int features;           // RT_FEAT_* present in the scene (selects the megakernel variant)
+    int need_dlen;          // |r.d| is used: media, metal / dielectric materials or the sky
     // camera (camera.h members)
     float org[3], llc[3], hor[3], ver[3], cu[3], cv[3];
     float lens, ct0, ct1;

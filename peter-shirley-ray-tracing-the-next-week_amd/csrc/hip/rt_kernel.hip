@@ -226,11 +226,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
 
         // ---- 4. media after the surfaces, then the hit record -------------------
         bool have = false;
+        // |r.d| once per segment, for the media and the specular materials / sky
+        const float dlen = (ready && A.need_dlen) ? len(r.d) : 0.f;
         Hit hr;
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            const int med_mat = media_hit<kCount, kInst>(A, lds_media, r, depth, g, have, best_t, cnt);
+            const int med_mat = media_hit<kCount, kInst>(A, lds_media, r, dlen, depth, g, have, best_t, cnt);
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
 
         mark(2);
         // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
-        const ShadeOut so = shade<kCount, kUV, kChecker>(A, ready, have, r, hr, depth, g, slots, lane, cnt);
+        const ShadeOut so = shade<kCount, kUV, kChecker>(A, ready, have, r, dlen, hr, depth, g, slots, lane, cnt);
         if (ready) {
             if (so.scattered) {
                 beta = mul(beta, so.att);

@@ -301,12 +301,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 g.mkey = (uint64_t)rg.z | ((uint64_t)rg.w << 32);
             }
             // media after the surfaces (constant_medium.h:26-50), then the record
+            const float dlen = (ready && A.need_dlen) ? len(r.d) : 0.f;
             bool have = false;
             Hit hr;
             hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
             if (ready) {
                 have = best_prim != kNone;
-                const int med_mat = media_hit<kCount>(A, lds_media, r, depth, g, have, best_t, cnt);
+                const int med_mat = media_hit<kCount>(A, lds_media, r, dlen, depth, g, have, best_t, cnt);
                 if (med_mat >= 0) {
                     hr.p = at(r, best_t);
                     hr.n = mk(1, 0, 0);
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                     hr = prim_record(A.prims, A.insts, A.mats, best_prim, r, best_t);
                 }
             }
-            ShadeOut so = shade<kCount>(A, ready, have, r, hr, depth, g, slots, lane, cnt);
+            ShadeOut so = shade<kCount>(A, ready, have, r, dlen, hr, depth, g, slots, lane, cnt);
             if (ready) {
                 if (so.scattered) {
                     beta = mul(beta, so.att);

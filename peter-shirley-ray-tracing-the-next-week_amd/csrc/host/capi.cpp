@@ -103,6 +103,7 @@ struct rt_scene {
     bool has_moving = false;
     bool has_uv = false;       // a material reads (u, v)
     bool has_checker = false;  // a checker_texture exists
+    bool has_specular = false; // a metal or dielectric material exists
     float time0 = 0, time1 = 1;
     // job cache
     std::vector<int32_t> job_tiles;
@@ -299,6 +300,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         }
         o.flags = (m.texture >= 0 && reads_uv(m.texture)) ? 1 : 0;
         s->has_uv |= o.flags != 0;
+        s->has_specular |= m.kind == RT_MAT_METAL || m.kind == RT_MAT_DIELECTRIC;
     }
     std::vector<rt_dtexture> texs(d->ntextures);
     for (int i = 0; i < d->ntextures; i++) {
@@ -478,6 +480,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.bvh_width = s->bvh_width;
     a.has_bvh = s->has_bvh;
     a.nmedia = s->nmedia;
+    a.need_dlen = s->nmedia > 0 || s->has_specular || p->background == RT_BG_SKY;
     a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
                  (s->has_checker ? RT_FEAT_CHECKER : 0);
     for (int k = 0; k < 3; k++) {
