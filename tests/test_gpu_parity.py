@@ -233,6 +233,19 @@ def test_default_work_item_is_one_sample_in_reference_order():
     assert (gamma_rms(a, o) <= TOL_RMS).all()
 
 
+def test_large_job_doubles_the_chunk_and_keeps_parity():
+    """Past the 8 GiB partial-sum slab (16 B x pixels x samples per item) the default
+    work item holds 2 samples (capi.cpp): 1000 x 1000 x 600 spp = 600 M samples.
+    Checked on sampled crops against the oracle with the same chunk."""
+    nx, ny, ns = 1000, 1000, 600
+    g, st = gpu_render("cornell_box", nx, ny, ns, seed=31, chunk=0, stats=True)
+    assert st["chunk"] == 2
+    assert np.isfinite(g).all() and (g >= 0).all()
+    for x0, y0 in ((0, 0), (496, 508), (992, 992)):
+        o = oracle_render("cornell_box", nx, ny, ns, seed=31, chunk=2, rect=(x0, y0, 8, 8))
+        assert (gamma_rms(g[y0:y0 + 8, x0:x0 + 8], o) <= TOL_RMS).all()
+
+
 @pytest.mark.parametrize("claim", ["1", "3", "16"])
 def test_claim_size_does_not_change_the_image(monkeypatch, claim):
     """Work items per wave-level claim (RTNW_CLAIM x 64) only change which lane runs
