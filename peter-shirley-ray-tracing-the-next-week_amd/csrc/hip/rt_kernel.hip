@@ -14,12 +14,14 @@
 //     regenerates a new camera sample as soon as its path terminates, so lanes stay
 //     busy across bounces (path regeneration) instead of idling until the longest
 //     path of the wave finishes;
-//   * work = (chunk of `chunk` samples) x (pixel); a wave claims A.claim (<= 512)
+//   * work = (chunk of `chunk` samples) x (pixel), one sample by default (short items
+//     keep a wave's lanes on neighbouring pixels); a wave claims A.claim (<= 512)
 //     work items per atomic (one global atomic per claim) and hands them
 //     to the lanes that need work with a ballot + mbcnt prefix count;
 //   * each item's radiance is summed in registers and stored once into a partial-sum
 //     slab [chunk][pixel]; rt_resolve sums the chunks in order (deterministic, no
-//     float atomics, independent of the number of GPUs);
+//     float atomics, independent of the number of GPUs; with one sample per item
+//     it is the reference's own `col += temp` order);
 //   * the BVH traversal stack lives in LDS, laid out [wave][depth][lane] so every
 //     push/pop of a wave is one conflict-free ds_write_b32/ds_read_b32;
 //   * nodes, primitives and materials are 16-B records read with dwordx4 loads.
@@ -32,8 +34,8 @@
 namespace {
 
 // Minimum waves per SIMD the register allocation must allow (launch_bounds second
-// argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  Traversal is latency-bound, so
-// occupancy wins over the few spilled dwords: tools/ab.py, profiles/r01.
+// argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  5 waves (96 VGPRs) spill 63
+// VGPRs and run 24% slower.
 
 // Shade once this many lanes of a wave have their closest hit (see stage 3).
 #ifndef RT_READY_BATCH
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         mark(0);
         if (kCount && first_active()) cnt.w_iters++;
 
-        // ---- 3. closest surface hit: BVH4 traversal rounds -------------------
+        // ---- 3. closest surface hit: BVH traversal rounds --------------------
         // A round = descend until every lane holds a leaf, test the leaves.  The
         // wave keeps running rounds for the lanes still searching until
         // RT_READY_BATCH lanes have their hit, then shades that batch: a lane that
