@@ -50,7 +50,7 @@ if args.fullres:
         for nx, ny in ({bench.image_for(n), wide_image(n)}):
             spp = args.spp // n
             cam = rtnw.Camera.preset("cornell", nx, ny)
-            params = rtnw.RenderParams(nx, ny, spp, max_depth=50, chunk=16, seed=2024)
+            params = rtnw.RenderParams(nx, ny, spp, max_depth=50, seed=2024)
             out = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
             stream = torch.cuda.current_stream(dev).cuda_stream
             t = sorted(scene.render_tiles(cam, params, [(0, 0, nx, ny)], out.data_ptr(), stream)["kernel_ms"]
@@ -63,7 +63,7 @@ base = None
 for n in [int(x) for x in args.ranks.split(",")]:
     nx, ny = wide_image(n) if args.wide else bench.image_for(n)
     cam = rtnw.Camera.preset("cornell", nx, ny)
-    params = rtnw.RenderParams(nx, ny, args.spp, max_depth=50, chunk=16, seed=2024)
+    params = rtnw.RenderParams(nx, ny, args.spp, max_depth=50, seed=2024)
     tiles, counts = rtnw.rank_layout(nx, ny, args.tile, n, args.order) if n > 1 else ([[(0, 0, nx, ny)]], [nx * ny * 3])
     out = torch.zeros(max(counts), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
