@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -42,6 +43,48 @@ int upload(void **dst, const std::vector<T> &v) {
     HIP_TRY(hipMalloc(dst, v.size() * sizeof(T)));
     HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     return RT_OK;
+}
+
+// The scene's arrays share one device allocation filled by one copy (scene creation
+// was a dozen hipMalloc + hipMemcpy round trips): stage() appends an array to the
+// host image at a 256-B aligned offset, commit() uploads it and sets the pointers.
+struct Arena {
+    std::vector<uint8_t> host;
+    std::vector<std::pair<void **, size_t>> fix;
+};
+template <class T>
+void stage(Arena &a, void **dst, const std::vector<T> &v) {
+    *dst = nullptr;
+    if (v.empty()) return;
+    const size_t off = (a.host.size() + 255) & ~(size_t)255, bytes = v.size() * sizeof(T);
+    a.host.resize(off + bytes);
+    std::memcpy(a.host.data() + off, v.data(), bytes);
+    a.fix.push_back({dst, off});
+}
+int commit(Arena &a, void **base) {
+    *base = nullptr;
+    if (a.host.empty()) return RT_OK;
+    HIP_TRY(hipMalloc(base, a.host.size()));
+    HIP_TRY(hipMemcpy(*base, a.host.data(), a.host.size(), hipMemcpyHostToDevice));
+    for (auto &f : a.fix) *f.first = (uint8_t *)*base + f.second;
+    return RT_OK;
+}
+
+// Resident workgroups per CU of the megakernel and the wavefront engine, per launch
+// mode and BVH width: a property of the code objects, queried once per process.
+hipError_t occupancy(int *mega, int *wave, int mode, int width) {
+    static std::mutex mu;
+    static int cache[3][2][2] = {};
+    std::lock_guard<std::mutex> lock(mu);
+    int *c = cache[mode][width == 4 ? 1 : 0];
+    if (!c[0]) {
+        hipError_t e;
+        if ((e = rt_megakernel_occupancy(&c[0], mode, width)) != hipSuccess) return e;
+        if ((e = rt_wavefront_occupancy(&c[1], mode, width)) != hipSuccess) { c[0] = 0; return e; }
+    }
+    *mega = c[0];
+    *wave = c[1];
+    return hipSuccess;
 }
 
 int ibits(float f) { int i; std::memcpy(&i, &f, 4); return i; }
@@ -95,7 +138,8 @@ struct rt_scene {
     int grid[3] = {0, 0, 0};      // persistent megakernel grid per variant (plain, count, profile)
     int grid_wf[3] = {0, 0, 0};   // persistent wavefront-engine grid per variant
     hipStream_t own_stream = nullptr;
-    // scene in HBM
+    // scene in HBM: one allocation (arena) holding the arrays below
+    void *arena = nullptr;
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
          *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr;
     uint32_t root = 0;
@@ -228,8 +272,7 @@ static int validate_desc(const rt_scene_desc *d) {
 void rt_scene_destroy(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    for (void *p : {s->wf, s->nodes, s->prims, s->bprims, s->media, s->mats, s->texs, s->insts, s->ranvec, s->perm, s->texels, s->job_xy,
-                    s->job_out, s->slab, s->counter, s->stats, s->host_out})
+    for (void *p : {s->wf, s->arena, s->job_xy, s->job_out, s->slab, s->counter, s->host_out})
         if (p) (void)hipFree(p);
     for (auto &e : s->ev) if (e) (void)hipEventDestroy(e);
     if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
@@ -240,11 +283,22 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     if (!out) return fail(RT_ERR_INVALID, "rt_scene_create: null out");
     *out = nullptr;
     if (int rc = validate_desc(d)) return rc;
+    // RTNW_TRACE: per-phase times of the scene setup on stderr (diagnostics)
+    const bool trace_on = std::getenv("RTNW_TRACE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto trace = [&](const char *what) {
+        if (!trace_on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "rt_scene_create: %-28s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev == 0) return fail(RT_ERR_HIP, "no HIP device available (the path tracer has no CPU fallback)");
     if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "device index out of range");
     HIP_TRY(hipSetDevice(device));
+    trace("device check");
 
     rtnw::BvhResult bvh;
     try {
@@ -252,6 +306,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     } catch (const std::exception &ex) {
         return fail(RT_ERR_INVALID, std::string("BVH build failed: ") + ex.what());
     }
+    trace("BVH build");
 
     auto *s = new rt_scene();
     s->device = device;
@@ -342,12 +397,21 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     std::vector<uint8_t> texels(d->image_data, d->image_data + (d->nimages > 0 ? d->image_bytes : 0));
     for (int v : perm) if (v < 0 || v > 255) return cleanup(fail(RT_ERR_INVALID, "Perlin permutation entry out of range"));
 
-    int rc;
-    if ((rc = bvh.width == 4 ? upload(&s->nodes, bvh.nodes4) : upload(&s->nodes, bvh.nodes2)) || (rc = upload(&s->prims, prims)) || (rc = upload(&s->bprims, bprims)) ||
-        (rc = upload(&s->media, media)) || (rc = upload(&s->mats, mats)) || (rc = upload(&s->texs, texs)) ||
-        (rc = upload(&s->insts, insts)) || (rc = upload(&s->ranvec, ranvec)) || (rc = upload(&s->perm, perm)) ||
-        (rc = upload(&s->texels, texels)))
-        return cleanup(rc);
+    Arena arena;
+    if (bvh.width == 4) stage(arena, &s->nodes, bvh.nodes4);
+    else stage(arena, &s->nodes, bvh.nodes2);
+    stage(arena, &s->prims, prims);
+    stage(arena, &s->bprims, bprims);
+    stage(arena, &s->media, media);
+    stage(arena, &s->mats, mats);
+    stage(arena, &s->texs, texs);
+    stage(arena, &s->insts, insts);
+    stage(arena, &s->ranvec, ranvec);
+    stage(arena, &s->perm, perm);
+    stage(arena, &s->texels, texels);
+    trace("device records");
+    if (int rc = commit(arena, &s->arena)) return cleanup(rc);
+    trace("upload (one allocation)");
     s->root = bvh.root;
     s->has_bvh = d->nprims > 0;
     s->nmedia = d->nmedia;
@@ -357,28 +421,30 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->nprims = d->nprims;
     s->ninstances = d->ninstances;
 
-    hipDeviceProp_t prop;
-    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return cleanup(hip_fail(e, "hipGetDeviceProperties"));
-    s->cus = prop.multiProcessorCount;
+    if ((e = hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+        return cleanup(hip_fail(e, "hipDeviceGetAttribute"));
     for (int mode = 0; mode < 3; mode++) {
-        int bpc = 0;
-        if ((e = rt_megakernel_occupancy(&bpc, mode, s->bvh_width)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+        int bpc = 0, wbpc = 0;
+        if ((e = occupancy(&bpc, &wbpc, mode, s->bvh_width)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
         // RTNW_BLOCKS_PER_CU caps the resident workgroups per CU (occupancy experiments only)
-        if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) bpc = std::min(bpc, std::max(1, std::atoi(e)));
+        if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) {
+            bpc = std::min(bpc, std::max(1, std::atoi(e)));
+            wbpc = std::min(wbpc, std::max(1, std::atoi(e)));
+        }
         s->grid[mode] = std::max(1, bpc) * s->cus;
-        int wbpc = 0;
-        if ((e = rt_wavefront_occupancy(&wbpc, mode, s->bvh_width)) != hipSuccess)
-            return cleanup(hip_fail(e, "occupancy query"));
-        if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) wbpc = std::min(wbpc, std::max(1, std::atoi(e)));
         s->grid_wf[mode] = std::max(1, wbpc) * s->cus;
     }
-    if ((e = hipMalloc(&s->counter, 64)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc counter"));
-    if ((e = hipMalloc(&s->stats, (RT_CNT_N + 16) * sizeof(unsigned long long))) != hipSuccess)
-        return cleanup(hip_fail(e, "hipMalloc stats"));
+    trace("device attributes");
+    // the work counter (64 B) and the statistics counters in one allocation
+    if ((e = hipMalloc(&s->counter, 64 + (RT_CNT_N + 16) * sizeof(unsigned long long))) != hipSuccess)
+        return cleanup(hip_fail(e, "hipMalloc counters"));
+    s->stats = (uint8_t *)s->counter + 64;
+    trace("counters");
     for (auto &ev : s->ev)
         if ((e = hipEventCreate(&ev)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
-    if ((e = hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking)) != hipSuccess)
-        return cleanup(hip_fail(e, "hipStreamCreate"));
+    trace("events");
+    // the scene's own stream (rt_render_tile's host-buffer path) is created on first
+    // use: creating a stream next to a framework's can take milliseconds
     *out = s;
     return RT_OK;
 }
@@ -610,6 +676,7 @@ int rt_render_tile(rt_scene *s, const rt_camera_desc *cam, const rt_render_param
         HIP_TRY(hipMalloc(&s->host_out, bytes));
         s->host_out_bytes = bytes;
     }
+    if (!s->own_stream) HIP_TRY(hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking));
     const int32_t tile[4] = {x0, y0, w, h};
     rt_stats local;
     if (int rc = rt_render_tiles(s, cam, p, tile, 1, (float *)s->host_out, s->own_stream, stats ? stats : &local)) return rc;
