@@ -662,6 +662,60 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
     return res;
 }
 
+// coop_reject for a wave whose requesting lanes need different samplers: lanes
+// with `disk` true want random_in_unit_disk (2 draws per candidate, camera.h:6-12),
+// the others random_in_unit_sphere (3 draws, material.h:41-47).  The owner
+// publishes its draw count per candidate beside its stream position, every lane
+// evaluates three draws and tests the candidate the way its owner's loop would (a
+// disk candidate's third draw is never used, and its z is 0 as in the reference),
+// and each owner advances its stream by its own count: the points and draws are
+// exactly those of coop_reject<2> / coop_reject<3>.  Lets the megakernel run the
+// lens-disk candidates of new camera samples in the shading stage's rounds.
+template <bool kCount>
+__device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, CoopSlot *slots, uint32_t lane,
+                                                Counters &cnt) {
+    V3 res = mk(0, 0, 0);
+    bool pending = want;
+    const uint32_t K = disk ? 2u : 3u;
+    uint64_t U = __ballot(pending);
+    while (U != 0ull) {
+        const uint32_t m = (uint32_t)__popcll(U);            // wave-uniform
+        const uint32_t inv = kCoop.inv[m];
+        const uint64_t P = kCoop.stride_mask[m];               // lanes congruent to 0 mod m
+        const uint32_t r = lanes_below(U);
+        if (pending) { slots[r].ctr = g.ctr; slots[r].pad = K; }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t t = (lane * inv) >> 16;                 // lane / m
+        const uint32_t slot = lane - t * m;
+        const uint32_t kk = (uint32_t)slots[slot].pad;
+        const uint64_t base = slots[slot].ctr + (uint64_t)(kk * t) * kGamma;
+        const double x = u48(mix64(base + kGamma)), y = u48(mix64(base + 2 * kGamma)), z = u48(mix64(base + 3 * kGamma));
+        const float pz = kk == 3u ? 2.0f * (float)z - 1.0f : 0.0f;
+        const V3 p = mk(2.0f * (float)x - 1.0f, 2.0f * (float)y - 1.0f, pz);
+        const uint64_t okm = __ballot((double)dot(p, p) < 1.0);
+        if (kCount && first_active()) cnt.w_rius++;
+        uint32_t src = lane;
+        bool won = false;
+        if (pending) {
+            const uint64_t win = okm & (P << r);
+            won = win != 0ull;
+            src = won ? (uint32_t)__builtin_ctzll(win) : lane;
+            const uint32_t tried = ((won ? src : 63u - r) * inv >> 16) + 1u;
+            g.ctr += (uint64_t)(K * tried) * kGamma;
+            if (kCount) cnt.l_rius += tried;
+            pending = !won;
+        }
+        const float qx = __shfl(p.x, (int)src), qy = __shfl(p.y, (int)src), qz = __shfl(p.z, (int)src);
+        if (won) res = mk(qx, qy, qz);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        U = __ballot(pending);
+    }
+    return res;
+}
+
 // Cooperative turbulence (perlin.h:64-74).  Octave k of turb(q) is
 // noise(q * 2^k) weighted 2^-k: `temp_p *= 2` and `weight *= 0.5` are exact, so
 // the octaves are independent.  The lanes that need turb publish q in LDS and the
@@ -847,40 +901,45 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
 }
 
 // ------------------------------------------------------------------ shade
-// color() at one hit (main.cpp:27-45) and material::scatter (material.h).
-// Lanes with `ready` false only help the cooperative samplers.  The per-material
-// work that dominates (texture lookup, the rejection loop of
-// random_in_unit_sphere) runs ONCE for every lane that needs it instead of once
-// per material branch; each lane still makes exactly the draws its own material
-// makes, in the same order (one material per lane).  No hit: `emitted` is the
-// background.  Must be called with all 64 lanes of the wave active.
 struct ShadeOut {
     bool scattered;
     V3 att, emitted;
     Ray ray;
 };
+
+// shade() in three parts, so that the megakernel can run other lanes' rejection
+// candidates in the same cooperative rounds (shade_begin -> coop -> shade_finish).
+struct ShadeState {
+    int kind;           // material kind (-1: no shading)
+    bool live;          // depth < max_depth (main.cpp:34)
+    bool wants_sphere;  // needs random_in_unit_sphere
+    V3 tv;              // texture value (lambertian / isotropic / light)
+};
+
+// Material, depth test, texture value incl. cooperative turbulence (textures
+// texture.h / perlin.h).  Must be called with all 64 lanes of the wave active.
 template <bool kCount, bool kUV = true, bool kChecker = true>
-// dlen = |r.d|, computed once per segment and shared with the media (RtKernelArgs.need_dlen).
-__device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, bool have, const Ray &r, float dlen,
-                                          const Hit &hr, int depth, Rng &g, CoopSlot *slots, uint32_t lane,
-                                          Counters &cnt) {
+__device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool ready, bool have, const Hit &hr, int depth,
+                                                  CoopSlot *slots, uint32_t lane, Counters &cnt) {
     const bool shading = ready && have;
-    int kind = -1;
-    bool live = false, noisy = false;
+    ShadeState st;
+    st.kind = -1;
+    st.live = false;
+    st.tv = mk(0, 0, 0);
+    bool noisy = false;
     float nscale = 0.f;
-    V3 tv = mk(0, 0, 0);
     if (shading) {
         if (kCount) cnt.shades++;
-        kind = fbits(A.mats[hr.mat * 2 + 0].x);
-        live = depth < A.max_depth;
-        const bool textured = kind == RT_MAT_DIFFUSE_LIGHT ||
-                              (live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_ISOTROPIC));
+        st.kind = fbits(A.mats[hr.mat * 2 + 0].x);
+        st.live = depth < A.max_depth;
+        const bool textured = st.kind == RT_MAT_DIFFUSE_LIGHT ||
+                              (st.live && (st.kind == RT_MAT_LAMBERTIAN || st.kind == RT_MAT_ISOTROPIC));
         if (textured) {
             float4 t0, t1;
             const int tkind = tex_leaf<kChecker>(A, fbits(A.mats[hr.mat * 2 + 0].y), hr.p, t0, t1);   // texture.h:35-44
             noisy = tkind == RT_TEX_NOISE;
             nscale = t0.w;
-            if (!noisy) tv = tex_value_leaf<kUV>(A, tkind, t0, t1, hr.u, hr.v);
+            if (!noisy) st.tv = tex_value_leaf<kUV>(A, tkind, t0, t1, hr.u, hr.v);
         }
     }
     if (kCount && noisy) cnt.noise++;
@@ -888,39 +947,57 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
     if (noisy) {                                                                               // texture.h:52-56
         const float sv = 1 + sinf(nscale * hr.p.x + 5 * turb);
         const float h = 0.5f * 1;
-        tv = mk(sv * h, sv * h, sv * h);
+        st.tv = mk(sv * h, sv * h, sv * h);
     }
-    const bool wants_sphere = shading && live && (kind == RT_MAT_LAMBERTIAN || kind == RT_MAT_METAL ||
-                                                  kind == RT_MAT_ISOTROPIC);
-    const V3 rius = coop_reject<3, kCount>(wants_sphere, g, slots, lane, cnt, SphereCand());   // material.h:41-47
+    st.wants_sphere = shading && st.live && (st.kind == RT_MAT_LAMBERTIAN || st.kind == RT_MAT_METAL ||
+                                             st.kind == RT_MAT_ISOTROPIC);
+    return st;
+}
+
+// The path ends at this segment whatever the scatter draws: a miss, a light, or
+// the depth limit (only metal can still end after its rius, material.h:81).
+__device__ __forceinline__ bool shade_ends(bool ready, bool have, const ShadeState &st) {
+    return ready && (!have || !st.live || st.kind == RT_MAT_DIFFUSE_LIGHT);
+}
+
+// emitted() of the segment: the background on a miss (TNW/Chapter03:29-31 for the
+// sky), the light's texture, else black.
+__device__ __forceinline__ V3 shade_emitted(const RtKernelArgs &A, bool have, const Ray &r, float dlen,
+                                            const ShadeState &st) {
+    if (!have) {
+        if (A.background != RT_BG_SKY) return mk(0, 0, 0);
+        const V3 ud = divs(r.d, dlen);   // unit(r.d), vec3.h:146
+        const float t = (float)(0.5 * ((double)ud.y + 1.0));
+        return add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
+    }
+    return st.kind == RT_MAT_DIFFUSE_LIGHT ? st.tv : mk(0, 0, 0);
+}
+
+// material::scatter (material.h) given the lane's random_in_unit_sphere point.
+// dlen = |r.d|, computed once per segment and shared with the media (RtKernelArgs.need_dlen).
+__device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool ready, bool have, const Ray &r, float dlen,
+                                                 const Hit &hr, const ShadeState &st, V3 rius, Rng &g) {
     ShadeOut o;
     o.scattered = false;
     o.att = mk(0, 0, 0);
     o.emitted = mk(0, 0, 0);
     o.ray = r;
-    // unit(r.d) (vec3.h:146) once, for the lanes whose shading needs it — metal,
-    // dielectric, the sky — instead of once in each of their branches
-    const bool wants_unit = ready && (have ? live && (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC)
-                                           : A.background == RT_BG_SKY);
+    const int kind = st.kind;
+    // unit(r.d) (vec3.h:146) once, for the lanes whose scatter needs it (metal,
+    // dielectric) instead of once in each of their branches
+    const bool wants_unit = ready && have && st.live && (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC);
     V3 ud = mk(0, 0, 0);
     if (wants_unit) ud = divs(r.d, dlen);
     if (!ready) return o;
-    if (!have) {
-        if (A.background == RT_BG_SKY) {                                  // TNW/Chapter03:29-31
-            float t = (float)(0.5 * ((double)ud.y + 1.0));
-            o.emitted = add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
-        }
-        return o;
-    }
+    o.emitted = shade_emitted(A, have, r, dlen, st);
+    if (!have || !st.live) return o;
     const float4 m0 = A.mats[hr.mat * 2 + 0];
     const float4 m1 = A.mats[hr.mat * 2 + 1];
-    o.emitted = kind == RT_MAT_DIFFUSE_LIGHT ? tv : mk(0, 0, 0);
-    if (!live) return o;
     Ray ns = r;
     if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
         V3 target = add(add(hr.p, hr.n), rius);
         ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;
-        o.att = tv;
+        o.att = st.tv;
         o.scattered = true;
     } else if (kind == RT_MAT_METAL) {                            // material.h:77-82
         V3 reflected = reflect(ud, hr.n);
@@ -963,11 +1040,27 @@ __device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, boo
         o.scattered = true;
     } else if (kind == RT_MAT_ISOTROPIC) {                        // material.h:145-149
         ns.o = hr.p; ns.d = rius; ns.time = 0.0f;
-        o.att = tv;
+        o.att = st.tv;
         o.scattered = true;
     }
     o.ray = ns;
     return o;
+}
+
+// color() at one hit (main.cpp:27-45) and material::scatter (material.h).
+// Lanes with `ready` false only help the cooperative samplers.  The per-material
+// work that dominates (texture lookup, the rejection loop of
+// random_in_unit_sphere) runs ONCE for every lane that needs it instead of once
+// per material branch; each lane still makes exactly the draws its own material
+// makes, in the same order (one material per lane).  No hit: `emitted` is the
+// background.  Must be called with all 64 lanes of the wave active.
+template <bool kCount, bool kUV = true, bool kChecker = true>
+__device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, bool have, const Ray &r, float dlen,
+                                          const Hit &hr, int depth, Rng &g, CoopSlot *slots, uint32_t lane,
+                                          Counters &cnt) {
+    const ShadeState st = shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt);
+    const V3 rius = coop_reject<3, kCount>(st.wants_sphere, g, slots, lane, cnt, SphereCand());   // material.h:41-47
+    return shade_finish(A, ready, have, r, dlen, hr, st, rius, g);
 }
 
 }  // namespace

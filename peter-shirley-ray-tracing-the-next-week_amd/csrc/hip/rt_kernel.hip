@@ -115,8 +115,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         if (kCount) cnt.segments++;
     };
 
-    for (;;) {
-        // ---- 1. retire a finished work item, claim new ones ------------------
+    // retire a finished work item (its sum to the slab), claim new ones for the lanes
+    // without work from the wave's pool (one global atomic per A.claim items)
+    auto retire_and_claim = [&]() {
         if (phase == PH_IDLE && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
             A.slab[item] = make_float4(part.x, part.y, part.z, 0.f);
             item = 0xFFFFFFFFu;
@@ -151,18 +152,18 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             need_mask = __ballot(need);
         }
         if (need) finished = true;
-        if (__ballot(!finished) == 0ull) break;
-
-        // ---- 2. start camera samples (main.cpp:305-308, camera.h:41-56) ------
-        const bool starting = phase == PH_IDLE && !finished;
-        float cu_ = 0, cv_ = 0;
+    };
+    // a camera sample (main.cpp:305-308, camera.h:41-56): the sample's stream and
+    // jitter, then (after the lens-disk point) the ray
+    auto camera_begin = [&](bool starting, float &cu_, float &cv_) {
         if (starting) {
             int j = A.ny - 1 - (int)py;
             g.start(sample_key(skey, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
             cu_ = (float)((double)(int)px + g.next()) / (float)A.nx;
             cv_ = (float)((double)j + g.next()) / (float)A.ny;
         }
-        const V3 disk = coop_reject<2, kCount>(starting, g, slots, lane, cnt, DiskCand());
+    };
+    auto camera_finish = [&](bool starting, float cu_, float cv_, V3 disk) {
         if (starting) {
             const CamView C = load_camera(lds_cam);
             V3 rd = scale(C.lens, disk);
@@ -177,6 +178,31 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             depth = 0;
             if (kCount) cnt.samples++;
             begin_segment();
+        }
+    };
+    // a path's radiance into its work item (de_nan, main.cpp:232-242; col += temp)
+    auto end_path = [&](V3 L) {
+        if (!(L.x == L.x)) L.x = 0;
+        if (!(L.y == L.y)) L.y = 0;
+        if (!(L.z == L.z)) L.z = 0;
+        part = add(part, L);
+        ++s_cur;
+        phase = PH_IDLE;
+    };
+
+    for (;;) {
+        // ---- 1. claims and camera samples for lanes without a path --------------
+        // (the first iteration, and paths that ended after the shading stage's
+        // cooperative rounds: a metal's absorbed reflection; the others start their
+        // next sample inside stage 5)
+        retire_and_claim();
+        if (__ballot(!finished) == 0ull) break;
+        {
+            const bool starting = phase == PH_IDLE && !finished;
+            float cu_ = 0, cv_ = 0;
+            camera_begin(starting, cu_, cv_);
+            const V3 disk = coop_reject<2, kCount>(starting, g, slots, lane, cnt, DiskCand());
+            camera_finish(starting, cu_, cv_, disk);
         }
         mark(0);
         if (kCount && first_active()) cnt.w_iters++;
@@ -246,23 +272,31 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
 
         mark(2);
         // ---- 5. shade (main.cpp:27-45, material.h) ------------------------------
-        const ShadeOut so = shade<kCount, kUV, kChecker>(A, ready, have, r, dlen, hr, depth, g, slots, lane, cnt);
-        if (ready) {
+        // Paths that end at this segment whatever the scatter draws (a miss, a light,
+        // the depth limit) add their radiance, retire, claim and draw their next camera
+        // sample's jitter right here, so that the new samples' lens-disk candidates run
+        // in the same cooperative rounds as the scattering lanes' sphere candidates.
+        const ShadeState st = shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt);
+        const bool ends = shade_ends(ready, have, st);
+        if (ends) end_path(mul(beta, shade_emitted(A, have, r, dlen, st)));
+        retire_and_claim();
+        const bool starting = phase == PH_IDLE && !finished;
+        float cu_ = 0, cv_ = 0;
+        camera_begin(starting, cu_, cv_);
+        // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
+        const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, lane, cnt);
+        if (ready && !ends) {
+            const ShadeOut so = shade_finish(A, ready, have, r, dlen, hr, st, pt, g);
             if (so.scattered) {
                 beta = mul(beta, so.att);
                 r = so.ray;
                 ++depth;
                 begin_segment();
             } else {
-                V3 L = mul(beta, so.emitted);
-                if (!(L.x == L.x)) L.x = 0;                                       // de_nan, main.cpp:232-242
-                if (!(L.y == L.y)) L.y = 0;
-                if (!(L.z == L.z)) L.z = 0;
-                part = add(part, L);
-                ++s_cur;
-                phase = PH_IDLE;
+                end_path(mul(beta, so.emitted));
             }
         }
+        camera_finish(starting, cu_, cv_, pt);
         mark(3);
     }
     if (kProf && lane == 0)
