@@ -67,6 +67,17 @@ def image_for(n, w=500, h=500):
     return round(w * k), round(h * k)
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(budget_procs, scene_name, nx, ny, target_s=8.0):
     """Reference renderer (oracle/_ref/ref_render, compiled from the reference's own
     sources) on host cores, rows split over P processes: a 1-spp pass calibrates the
@@ -91,6 +102,7 @@ def cpu_baseline(budget_procs, scene_name, nx, ny, target_s=8.0):
             ok, dt = run(ns)
             if ok:
                 return {"value": nx * ny * ns / dt / 1e6, "unit": "Msamples/s", "cores": P, "kind": "reference",
+                        "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
                         "sample": f"{scene_name}() {nx}x{ny}x{ns}spp (spp sized by a 1-spp pass), the reference's "
                                   f"own accelerator choice (final(): flat list as shipped, main.cpp:291), rows split "
                                   f"over {P} processes of oracle/_ref/ref_render (clang++ -O2), wall {dt:.2f}s"}
@@ -100,6 +112,7 @@ def cpu_baseline(budget_procs, scene_name, nx, ny, target_s=8.0):
     spec = O.kernel_spec(scene_name, nx, ny, ns, seed=0, threads=P)
     _, st = O.render(spec)
     return {"value": st["samples"] / st["seconds"] / 1e6, "unit": "Msamples/s", "cores": P, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{scene_name}() {nx}x{ny}x{ns}spp, oracle/rt_oracle.c, OpenMP {P} threads, "
                       f"{st['seconds']:.2f}s"}
 
