@@ -527,8 +527,8 @@ __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, fl
 }
 
 // One traversal round's descent (both engines).  A lane that reaches a leaf
-// postpones it (pleaf) and keeps descending speculatively until every lane holds a
-// leaf or has nothing left (Aila & Laine 2009), so node steps and leaf tests both
+// postpones it (pleaf) and keeps descending speculatively until the lanes hold a
+// leaf or have nothing left (Aila & Laine 2009), so node steps and leaf tests both
 // run with most lanes busy; culling against a not-yet-updated best_t is merely
 // conservative.  One branch per step (the node fetch): parking a leaf and popping
 // the stack are selects, the pop's LDS read unconditional (the exec-mask

@@ -208,7 +208,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
         if (kCount && first_active()) cnt.w_iters++;
 
         // ---- 3. closest surface hit: BVH traversal rounds --------------------
-        // A round = descend until every lane holds a leaf, test the leaves.  The
+        // A round = descend until all but RT_DESCEND_TAIL searching lanes hold a
+        // leaf, test the leaves.  The
         // wave keeps running rounds for the lanes still searching until
         // RT_READY_BATCH lanes have their hit, then shades that batch: a lane that
         // finished early no longer holds the wave in traversal, and a lane still

@@ -233,8 +233,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WF_WAVES_PER_SIMD) void rt_wavefront(R
                 }
                 if (__ballot(slot != kNone) == 0ull) break;
                 if (slot != kNone) {
-                    // one round: descend (speculatively past the first leaf) until
-                    // every lane holds a leaf, then test the leaves
+                    // one round: descend (speculatively past the first leaf) until all
+                    // but RT_DESCEND_TAIL lanes hold a leaf, then test the leaves
                     const uint32_t pleaf = descend<kWidth, kCount>(A.nodes, node, sl, best_t, stk, sp, cnt);
                     if (pleaf != RT_EMPTY_CHILD) {
                         const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
