@@ -282,7 +282,10 @@ def main():
                          "node_visits_per_ray": cst["node_visits"] / max(1.0, cst["segments"]),
                          "prim_tests_per_ray": (cst["sphere_tests"] + cst["moving_sphere_tests"] + cst["rect_tests"])
                          / max(1.0, cst["segments"]),
-                         "algorithmic_bytes_per_sample": alg / max(1.0, cst["samples"])},
+                         "algorithmic_bytes_per_sample": alg / max(1.0, cst["samples"]),
+                         "note": "algorithmic bytes count every node/primitive fetch; the scene is L2-resident, so "
+                                 "frac > 1 is possible and the kernel is VALU-issue bound (DESIGN.md 5c); "
+                                 "traffic = PMC HBM bytes per launch (profiles/r01/traffic.json)"},
             "cpu_baseline": None,
         }
         if world == 1:
