@@ -220,7 +220,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             if (phase == PH_TRAV) {
                 // the slab test needs no exact division: boxes are padded (bvh.cpp)
                 const Slab sl = make_slab(r, A.tmin);
-                const uint32_t pleaf = descend<kWidth, kCount>(A.nodes, node, sl, best_t, stk, sp, cnt);
+                const uint32_t pleaf = descend<kWidth, kCount, kInst ? 1 : 2>(A.nodes, node, sl, best_t, stk, sp, cnt);
                 if (pleaf != RT_EMPTY_CHILD) {
                     const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
                     // primitives in pairs: both 32-B heads are fetched before either test
