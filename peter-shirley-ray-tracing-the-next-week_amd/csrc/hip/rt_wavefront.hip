@@ -28,7 +28,7 @@
 #include "rt_device.h"
 
 #ifndef RT_WF_WAVES_PER_SIMD
-#define RT_WF_WAVES_PER_SIMD 5
+#define RT_WF_WAVES_PER_SIMD 4
 #endif
 
 namespace {
