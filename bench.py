@@ -1,26 +1,40 @@
 #!/usr/bin/env python3
 """bench.py — Msamples/s of the final() path-tracing workload on MI355X.
 
-Workload (BASELINE.json configs[3], the metric's config): final() (main.cpp:190-230),
-camera main.cpp:254-259, 1000 spp, depth 50, black background, 500x500 pixels per
-GPU.  One step = one full render of the job: every pixel x every sample, camera
-ray -> path -> BVH/primitive/medium hits -> scatter, through the C ABI's
-persistent HIP megakernel, plus (N > 1) the RCCL gather of the packed tiles to
-rank 0.  Scene upload and BVH build happen before the timed region (inputs
-resident in HBM); the PPM write is not part of a step.
+One step = one full render of the job: every pixel x every sample, camera ray ->
+path -> BVH/primitive/medium hits -> scatter, through the C ABI's persistent HIP
+megakernel (rt_render_tiles, output left in HBM), plus for N > 1 the gather of the
+ranks' packed framebuffers to rank 0.  Scene upload and BVH build happen before the
+timed region (inputs resident in HBM); the PPM write is not part of a step.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling — N ranks render the same
-view at N x 250,000 pixels (square, side round(500 sqrt(N)): 500, 707, 1000 =
-config 5's image, 1414).  The pixels are interleaved over the ranks (N = a x b,
-rank (ry, rx) renders x = rx mod a, y = ry mod b: a sub-sampled copy of the whole
-view, so every rank's expected cost is the same), then one torch.distributed
-gather (backend "nccl" = RCCL over xGMI) of the packed float pixels to rank 0.  `--dist-backend gloo` gathers through host memory instead, so the
-multi-rank path can be rehearsed with several ranks on one GPU.
+Workloads (BASELINE.json configs):
+  N = 1 (default c4, the metric's config): final() (main.cpp:190-230), camera
+      main.cpp:254-259, 500 x 500 x 1000 spp, depth 50, black background.
+  N > 1 (default c5): final() 1000 x 1000 x 1000 spp split over the N ranks —
+      strong scaling, total work fixed (the config BASELINE quotes for 8 GPUs).
+      The pixels are interleaved over the ranks (N = a x b, rank (ry, rx) renders
+      x = rx mod a, y = ry mod b: a sub-sampled copy of the whole view, so every
+      rank's expected cost is the same), then ONE gather to rank 0: `--gather
+      torch` (default: torch.distributed.gather, backend "nccl" = RCCL) or
+      `--gather native` (the C ABI's rt_dist_gather = ncclGather on its own RCCL
+      communicator, rccl.h:745).  `--dist-backend gloo` gathers through host memory
+      so the multi-rank path can be rehearsed with several ranks on one GPU.
+  --config c2 / c3 / c4 with N > 1: weak scaling, N x the 1-GPU pixels.
 
-Prints ONE JSON line (rank 0) with roofline (algorithmic bytes / kernel time vs
-8 TB/s HBM) and cpu_baseline (the reference binary on host cores, bounded sample).
+Prints ONE JSON line (rank 0) with
+  roofline: the megakernel is bound by VALU instruction issue: the
+    wave-level VALU instructions of one launch (SQ_INSTS_VALU per sample from the
+    committed rocprofv3 pass, profiles/r<NN>/traffic.json, for this very library
+    build) over the kernel's live HIP-event time, against 1,024 SIMDs x 2.4 GHz / 2
+    cycles per wave64 VALU instruction; hbm_frac = PMC-measured HBM bytes per launch
+    over the same time vs 8 TB/s; cache_served_bytes = SURVEY §8d's byte model.
+  cpu_baseline: the reference binary (oracle/_ref/ref_render, compiled from the
+    reference's own sources) on this job's CPU cores, bounded sample; the flat list
+    as shipped (main.cpp:291) and with a corrected BVH (bvh.h:29-54, slab fixed).
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import subprocess
@@ -39,7 +53,10 @@ import torch.distributed as dist  # noqa: E402
 import rtnw  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-TILE = 8                       # unused by the interleaved layout
+SIMDS = 1024                   # 256 CUs x 4 SIMD-32 (MI355X_MICROARCH.md)
+CLOCK_GHZ = 2.4                # max engine clock (spec)
+VALU_CYCLES = 2                # a wave64 VALU instruction issues over 2 cycles on SIMD-32
+VALU_PEAK = SIMDS * CLOCK_GHZ * 1e9 / VALU_CYCLES   # wave-level VALU instructions / s
 METRIC = "Msamples/s (pixels×spp/s) + achieved HBM GB/s, final() 500×500×1000spp"   # BASELINE.json
 LAYOUT = "interleaved"         # rtnw.pixels_for_rank: rank (ry, rx) of a x b renders x = rx mod a, y = ry mod b
 
@@ -48,21 +65,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-# BASELINE.json configs on one GPU: scene, image, spp (depth / background / camera:
-# rtnw.SCENE_DEFAULTS).  c4 is the metric's config and the default; c2 and c3 are
-# reported with --config for DESIGN.md, never as the headline.
+# BASELINE.json configs: scene, image, spp, scaling over N (depth / background /
+# camera: rtnw.SCENE_DEFAULTS).  c4 is the metric's config and the 1-GPU default; c5
+# the multi-GPU default; c2 and c3 are reported with --config for DESIGN.md.
 CONFIGS = {
-    "c2": ("cornell_box", 400, 400, 200),
-    "c3": ("random_motion", 800, 400, 500),
-    "c4": ("final", 500, 500, 1000),
+    "c2": ("cornell_box", 400, 400, 200, "weak"),
+    "c3": ("random_motion", 800, 400, 500, "weak"),
+    "c4": ("final", 500, 500, 1000, "weak"),
+    "c5": ("final", 1000, 1000, 1000, "strong"),
 }
 
 
 def image_for(n, w=500, h=500):
-    """N x (w x h) pixels at the 1-GPU image's aspect and view: sides scaled by sqrt(N)
-    (final(): 500, 707, 1000 = config 5's image, 1414).  A wider image would show more
-    of the dark ground and cost ~18% less per sample (tools/scaling_probe.py
-    --fullres), so per-GPU work would shrink with N."""
+    """Weak scaling: N x (w x h) pixels at the 1-GPU image's aspect and view, sides
+    scaled by sqrt(N) (a wider image would show more of the dark ground and cost ~18%
+    less per sample, tools/scaling_probe.py --fullres)."""
     k = n ** 0.5
     return round(w * k), round(h * k)
 
@@ -78,60 +95,98 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(budget_procs, scene_name, nx, ny, target_s=8.0):
-    """Reference renderer (oracle/_ref/ref_render, compiled from the reference's own
-    sources) on host cores, rows split over P processes: a 1-spp pass calibrates the
-    sample count so the timed pass takes about `target_s` seconds."""
+def usable_cores():
+    """CPUs this job may use: the affinity mask, capped by the cgroup's CPU quota (the
+    GPU box gives a one-GPU job a 16-CPU quota on a 256-CPU host)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def ref_rate(scene_name, nx, ny, procs, accel, target_s):
+    """The reference binary on `procs` processes (row bands), a 1-spp pass sizing the
+    timed pass to about target_s seconds; returns (Msamples/s, spp, wall s)."""
     ref = os.path.join(ORACLE, "_ref", "ref_render")
-    P = budget_procs
     cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
+
+    def run(ns):
+        bands = [(ny * i // procs, ny * (i + 1) // procs) for i in range(procs)]
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen([ref, "--scene", scene_name, "--nx", str(nx), "--ny", str(ny), "--ns", str(ns),
+                                "--depth", str(depth), "--bg", "sky" if bg == rtnw.RT_BG_SKY else "black",
+                               "--cam", cam_name, "--rows", f"{a}:{b}", "--accel", accel],
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd="/tmp")
+              for a, b in bands if b > a]
+        ok = all(p.wait() == 0 for p in ps)
+        return ok, time.perf_counter() - t0
+
+    ok, dt1 = run(1)
+    if not ok:
+        return None
+    ns = max(1, min(1000, round(target_s / max(dt1, 1e-3))))
+    ok, dt = run(ns)
+    return (nx * ny * ns / dt / 1e6, ns, dt) if ok else None
+
+
+def cpu_baseline(scene_name, nx, ny, target_s=10.0):
+    """Reference renderer on every CPU this job may use: the flat list as shipped
+    (main.cpp:291) is `value`; the reference's own bvh_node with the slab test fixed
+    (--accel bvh, oracle/ref_harness.cpp fixed_bvh) is reported beside it."""
+    ref = os.path.join(ORACLE, "_ref", "ref_render")
+    P = usable_cores()
+    host = os.cpu_count()
     if os.path.exists(ref) and os.access(ref, os.X_OK):
-        def run(ns):
-            bands = [(ny * i // P, ny * (i + 1) // P) for i in range(P)]
-            t0 = time.perf_counter()
-            procs = [subprocess.Popen([ref, "--scene", scene_name, "--nx", str(nx), "--ny", str(ny), "--ns", str(ns),
-                                       "--depth", str(depth), "--bg", "sky" if bg == rtnw.RT_BG_SKY else "black",
-                                       "--cam", cam_name, "--rows", f"{a}:{b}"],
-                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd="/tmp")
-                     for a, b in bands]
-            ok = all(p.wait() == 0 for p in procs)
-            return ok, time.perf_counter() - t0
-        ok, dt1 = run(1)
-        if ok:
-            ns = max(1, min(1000, round(target_s / max(dt1, 1e-3))))
-            ok, dt = run(ns)
-            if ok:
-                return {"value": nx * ny * ns / dt / 1e6, "unit": "Msamples/s", "cores": P, "kind": "reference",
-                        "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-                        "sample": f"{scene_name}() {nx}x{ny}x{ns}spp (spp sized by a 1-spp pass), the reference's "
-                                  f"own accelerator choice (final(): flat list as shipped, main.cpp:291), rows split "
-                                  f"over {P} processes of oracle/_ref/ref_render (clang++ -O2), wall {dt:.2f}s"}
+        flat = ref_rate(scene_name, nx, ny, P, "flat", target_s)
+        bvh = ref_rate(scene_name, nx, ny, P, "bvh", target_s)
+        if flat:
+            res = {"value": flat[0], "unit": "Msamples/s", "cores": P, "kind": "reference",
+                   "cpu_model": cpu_model(), "host_cpus": host,
+                   "sample": f"{scene_name}() {nx}x{ny}x{flat[1]}spp (spp sized by a 1-spp pass), the reference as "
+                             f"shipped (final(): flat list, main.cpp:291), rows split over {P} processes of "
+                             f"oracle/_ref/ref_render (clang++ -O2) = this job's CPU quota, wall {flat[2]:.2f}s"}
+            if bvh:
+                res["corrected_bvh"] = {"value": bvh[0], "unit": "Msamples/s", "cores": P,
+                                        "sample": f"{scene_name}() {nx}x{ny}x{bvh[1]}spp, the reference's bvh_node "
+                                                  f"(bvh.h:29-54, 97-121) with aabb::hit's slab fixed, wall {bvh[2]:.2f}s"}
+            if host and host > P:
+                res["all_host_cpus_extrapolated"] = {
+                    "cpus": host, "flat": flat[0] * host / P, "corrected_bvh": bvh[0] * host / P if bvh else None,
+                    "note": "linear per-core extrapolation; this job may use only its quota"}
+            return res
     sys.path.insert(0, ORACLE)
     import oracle as O
     ns = 2
-    spec = O.kernel_spec(scene_name, nx, ny, ns, seed=0, threads=P)
-    _, st = O.render(spec)
+    _, st = O.render(O.kernel_spec(scene_name, nx, ny, ns, seed=0, threads=P))
     return {"value": st["samples"] / st["seconds"] / 1e6, "unit": "Msamples/s", "cores": P, "kind": "port",
-            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-            "sample": f"{scene_name}() {nx}x{ny}x{ns}spp, oracle/rt_oracle.c, OpenMP {P} threads, "
-                      f"{st['seconds']:.2f}s"}
+            "cpu_model": cpu_model(), "host_cpus": host,
+            "sample": f"{scene_name}() {nx}x{ny}x{ns}spp, oracle/rt_oracle.c, OpenMP {P} threads, {st['seconds']:.2f}s"}
 
 
-def read_traffic(samples_per_launch):
-    """HBM bytes per launch from the latest committed PMC measurement
-    (profiles/r<NN>/traffic.json, written by tools/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this workload, FETCH_SIZE doubled per
-    the gfx950 correction), scaled to this launch's sample count."""
-    import glob
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "traffic.json")))
-    if not found:
-        return None
-    try:
-        with open(found[-1]) as f:
-            t = json.load(f)
-        return t["hbm_bytes_per_sample"] * samples_per_launch
-    except Exception:
-        return None
+def lib_sha16():
+    with open(rtnw.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def read_profile(workload_key):
+    """The latest committed PMC summary (profiles/r<NN>/traffic.json, tools/pmc_traffic.py
+    from separate rocprofv3 passes of this workload): HBM bytes and VALU instructions
+    per sample of the timed megakernel, and the library build they were measured on."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if t.get("config", "c4") == workload_key:
+            t["path"] = os.path.relpath(path, ROOT)
+            return t
+    return None
 
 
 def end_to_end(scene_name, cam, params, nx, ny, dev):
@@ -161,12 +216,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="", choices=[""] + sorted(CONFIGS),
+                    help="default: c4 on one GPU, c5 (final() 1000^2 x 1000 spp, strong scaling) on several")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp")
-    ap.add_argument("--chunk", type=int, default=0, help="samples per work item; 0 = the C ABI's default (1 here)")
+    ap.add_argument("--chunk", type=int, default=0, help="samples per work item; 0 = the C ABI's default (1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ppm", default="")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--gather", default="torch", choices=["torch", "native"],
+                    help="torch.distributed.gather, or the C ABI's rt_dist_gather (ncclGather on its own RCCL comm)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,14 +237,16 @@ def main():
         dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", gpu)
 
-    scene_name, w1, h1, spp = CONFIGS[args.config]
+    cfg = args.config or ("c4" if world == 1 else "c5")
+    scene_name, w1, h1, spp, scaling = CONFIGS[cfg]
     spp = args.spp or spp
     cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
-    nx, ny = image_for(world, w1, h1)
+    nx, ny = (w1, h1) if scaling == "strong" else image_for(world, w1, h1)
     if world > 1:
-        all_tiles, all_counts = rtnw.rank_layout(nx, ny, TILE, world, LAYOUT)
+        all_tiles = [rtnw.pixels_for_rank(nx, ny, r, world) for r in range(world)]
     else:
-        all_tiles, all_counts = [[(0, 0, nx, ny)]], [nx * ny * 3]
+        all_tiles = [[(0, 0, nx, ny)]]
+    all_counts = [int(np.asarray(t).reshape(-1, 4)[:, 2:].prod(axis=1).sum()) * 3 for t in all_tiles]
     tiles = all_tiles[rank]
     n_max = max(all_counts)
 
@@ -194,19 +254,31 @@ def main():
     cam = rtnw.Camera.preset(cam_name, nx, ny)
     params = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, chunk=args.chunk, seed=2024)
     out = torch.zeros(n_max, dtype=torch.float32, device=dev)
-    gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    gather_list = [torch.empty(n_max, dtype=torch.float32, device=gdev) for _ in range(world)] \
-        if (world > 1 and rank == 0) else None
+    native = world > 1 and args.gather == "native"
+    comm = None
+    if native:   # the C ABI's own RCCL communicator; the unique id travels over the torch process group
+        obj = [rtnw.dist_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm = rtnw.Dist(obj[0], rank, world, gpu)
+        recv = torch.empty(world * n_max if rank == 0 else 1, dtype=torch.float32, device=dev)
+        gather_list = None
+    else:
+        gdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        gather_list = [torch.empty(n_max, dtype=torch.float32, device=gdev) for _ in range(world)] \
+            if (world > 1 and rank == 0) else None
 
     def step():
         stream = torch.cuda.current_stream(dev).cuda_stream
         st = scene.render_tiles(cam, params, tiles, out.data_ptr(), stream, stats=True)
-        if world > 1:
+        if native:
+            comm.gather(out.data_ptr(), n_max, recv.data_ptr(), 0, stream)
+        elif world > 1:
             dist.gather(out if args.dist_backend == "nccl" else out.cpu(), gather_list, dst=0)
         return st
 
-    workload = f"{args.config}: {scene_name}() {nx}x{ny} pixels x {spp} spp, depth {depth}" + \
-        (f" over {world} GPUs" if world > 1 else "")
+    workload = f"{cfg}: {scene_name}() {nx}x{ny} pixels x {spp} spp, depth {depth}" + \
+        (f", split over {world} GPUs" if world > 1 and scaling == "strong" else
+         (f", {world} GPUs x {nx * ny // world} pixels" if world > 1 else ""))
     for i in range(args.warmup):
         st = step()
         log(f"[rank {rank}] warmup {i}: kernel {st['kernel_ms']:.1f} ms")
@@ -219,14 +291,14 @@ def main():
     for i in range(args.steps):
         st = step()
         kms.append(st["kernel_ms"])
-        log(f"[rank {rank}] step {i}: kernel {st['kernel_ms']:.1f} ms")
+        log(f"[rank {rank}] step {i}: kernel {st['kernel_ms']:.1f} ms ({int(st['batches'])} launch(es))")
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -234,29 +306,59 @@ def main():
     value = samples_per_step * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the megakernel: algorithmic bytes (counting launch, same RNG -> same
-    # paths) over the average HIP-event duration of the timed launches on this rank
+    # roofline of this rank's megakernel launches (HIP events on the render stream)
+    rank_samples = all_counts[rank] // 3 * spp
+    avg_kernel_s = float(np.mean(kms)) / 1e3
     cnt = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, chunk=args.chunk, seed=2024,
                             flags=rtnw.RT_FLAG_COUNT)
     cst = scene.render_tiles(cam, cnt, tiles, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream, stats=True)
-    avg_kernel_s = float(np.mean(kms)) / 1e3
-    alg = cst["algorithmic_bytes"]
-    achieved = alg / avg_kernel_s / 1e9
+    cache_bytes = cst["algorithmic_bytes"]
+    prof = read_profile("c4" if cfg in ("c4", "c5") and scene_name == "final" else cfg)
+    sha = lib_sha16()
+    roof = {"bound": "valu_issue", "achieved": None, "peak": VALU_PEAK / 1e9, "unit": "G wave-VALU-instr/s",
+            "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
+            "batches_per_step": int(st["batches"]),
+            "valu_insts_per_sample": None, "profile": None, "profile_matches_library": None,
+            "cache_served_bytes_per_launch": cache_bytes,
+            "cache_served_bytes_per_sample": cache_bytes / max(1.0, cst["samples"]),
+            "cache_served_GBps": cache_bytes / avg_kernel_s / 1e9,
+            "rays_per_sample": cst["segments"] / max(1.0, cst["samples"]),
+            "node_visits_per_ray": cst["node_visits"] / max(1.0, cst["segments"]),
+            "prim_tests_per_ray": (cst["sphere_tests"] + cst["moving_sphere_tests"] + cst["rect_tests"])
+            / max(1.0, cst["segments"]),
+            "note": "the scene is L2/L1-resident: HBM carries ~1% of peak, the kernel is VALU-issue bound "
+                    "(DESIGN.md §5c).  achieved = SQ_INSTS_VALU per sample (committed rocprofv3 pass of this "
+                    "library build) x samples / live kernel time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles; "
+                    "traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE); cache_served = SURVEY "
+                    "§8d byte model (node/primitive fetches, mostly L1/L2 hits)"}
+    if prof:
+        roof["profile"] = prof["path"]
+        roof["profile_matches_library"] = prof.get("lib_sha16") == sha
+        if prof.get("valu_insts_per_sample"):
+            vi = prof["valu_insts_per_sample"] * rank_samples
+            roof["valu_insts_per_sample"] = prof["valu_insts_per_sample"]
+            roof["achieved"] = vi / avg_kernel_s / 1e9
+            roof["frac"] = vi / avg_kernel_s / VALU_PEAK
+        if prof.get("hbm_bytes_per_sample"):
+            tr = prof["hbm_bytes_per_sample"] * rank_samples
+            roof["traffic"] = tr
+            roof["hbm_frac"] = tr / avg_kernel_s / (HBM_PEAK_GBS * 1e9)
 
     if rank == 0 and args.ppm:
         if world == 1:
             img = out[: nx * ny * 3].cpu().numpy().reshape(ny, nx, 3)
-        else:   # the last timed step's gathered tiles, unpacked on the root
+        else:   # the last timed step's gathered shares, unpacked on the root
             img = np.zeros((ny, nx, 3), np.float32)
             for r in range(world):
-                rtnw.unpack_tiles(gather_list[r][: all_counts[r]].cpu().numpy(), all_tiles[r], img)
+                src = recv[r * n_max:(r + 1) * n_max] if native else gather_list[r]
+                rtnw.unpack_tiles(src[: all_counts[r]].cpu().numpy(), all_tiles[r], img)
         with open(args.ppm, "wb") as f:
             f.write(rtnw.ppm_text(rtnw.quantize(img)))
 
     if rank == 0:
         res = {
-            "metric": METRIC if args.config == "c4" else
-            f"Msamples/s (pixels×spp/s) + achieved HBM GB/s, {scene_name}() {w1}×{h1}×{CONFIGS[args.config][3]}spp",
+            "metric": METRIC if cfg == "c4" else
+            f"Msamples/s (pixels×spp/s) + achieved HBM GB/s, {scene_name}() {w1}×{h1}×{CONFIGS[cfg][3]}spp",
             "value": value,
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -264,7 +366,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic: procedural {scene_name}() scene built by the host API (main.cpp builders), "
@@ -272,27 +374,19 @@ def main():
             "config": {"workload": workload, "image": [nx, ny], "spp": spp, "pixels_per_gpu": nx * ny // world,
                        "rank_layout": ("pixel interleave %dx%d" % rtnw.interleave_factors(world)) if world > 1 else None,
                        "chunk": int(cst["chunk"]),
-                       "parallelism": f"pixels x{world}" + (" + RCCL gather" if world > 1 else "")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": read_traffic(nx * ny // world * spp) if args.config == "c4" else None,
-                         "kernel_ms_avg": avg_kernel_s * 1e3,
-                         "algorithmic_bytes_per_launch": alg,
-                         "rays_per_sample": cst["segments"] / max(1.0, cst["samples"]),
-                         "node_visits_per_ray": cst["node_visits"] / max(1.0, cst["segments"]),
-                         "prim_tests_per_ray": (cst["sphere_tests"] + cst["moving_sphere_tests"] + cst["rect_tests"])
-                         / max(1.0, cst["segments"]),
-                         "algorithmic_bytes_per_sample": alg / max(1.0, cst["samples"]),
-                         "note": "algorithmic bytes count every node/primitive fetch; the scene is L2-resident, so "
-                                 "frac > 1 is possible and the kernel is VALU-issue bound (DESIGN.md 5c); "
-                                 "traffic = PMC HBM bytes per launch (profiles/r01/traffic.json)"},
+                       "gather": (("rt_dist_gather (ncclGather)" if native else
+                                   f"torch.distributed.gather ({args.dist_backend})") if world > 1 else None),
+                       "parallelism": f"pixels x{world}" + (" + one gather" if world > 1 else "")},
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if world == 1:
             res["end_to_end"] = end_to_end(scene_name, cam, params, nx, ny, dev)
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(min(16, os.cpu_count() or 1), scene_name, w1, h1)
+            res["cpu_baseline"] = cpu_baseline(scene_name, w1, h1)
         print(json.dumps(res), flush=True)
+    if comm is not None:
+        comm.close()
     scene.close()
     if world > 1:
         dist.destroy_process_group()

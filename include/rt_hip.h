@@ -145,7 +145,16 @@ int rt_camera_init(rt_camera_desc *out, const float lookfrom[3], const float loo
 enum { RT_BG_BLACK = 0, RT_BG_SKY = 1 };
 enum {
     RT_FLAG_COUNT = 1,            /* counting variant: fills the rt_stats visit counters */
-    RT_FLAG_PROFILE = 2           /* stamp variant: fills cycles_* (diagnostic; never timed) */
+    RT_FLAG_PROFILE = 2,          /* stamp variant: fills cycles_* (diagnostic; never timed) */
+    /* Progressive rendering / checkpoint-resume: the output holds per-pixel
+     * SUMS instead of means.  SUM_IN: on entry the output already holds the sums of
+     * samples [0, sample_offset) (e.g. read back from rt_checkpoint_read); this call
+     * adds samples [sample_offset, sample_offset + spp) to them one at a time, in
+     * sample order, so a resumed render is bitwise the uninterrupted one.  SUM_OUT:
+     * write the sums (to checkpoint or resume later); without it the output is the
+     * mean, col * float(1.0 / ns) with ns = sample_offset + spp under SUM_IN, else spp. */
+    RT_FLAG_SUM_IN = 4,
+    RT_FLAG_SUM_OUT = 8
 };
 
 typedef struct rt_render_params {
@@ -154,8 +163,13 @@ typedef struct rt_render_params {
     int32_t max_depth;            /* scatter while depth < max_depth (main.cpp:34: 50) */
     float t_min;                  /* main.cpp:27: 0.001 */
     int32_t background;           /* RT_BG_* */
-    int32_t chunk;                /* samples per partial sum; <= 0 selects 1, doubled while the
-                                     slab (16 B x pixels x ceil(spp/chunk)) would pass 8 GiB */
+    int32_t chunk;                /* samples per work item (partial sum); <= 0 selects 1, the
+                                     reference's one-add-per-sample order (main.cpp:311).  A job
+                                     whose partial-sum slab (16 B x pixels x ceil(spp/chunk))
+                                     would pass the slab budget (8 GiB, env RTNW_SLAB_BUDGET) runs
+                                     as several launches over sample batches, each batch added
+                                     to a per-pixel running sum in sample order: the image does
+                                     not depend on the job's size or split (any rank count) */
     int32_t flags;                /* RT_FLAG_* */
     uint32_t sample_offset;       /* first sample index (progressive rendering) */
     uint32_t pad;
@@ -187,6 +201,7 @@ typedef struct rt_stats {
     double wave_sphere_draw_trips;/*   wave-level random_in_unit_sphere rejection rounds */
     double lane_sphere_draw_trips;/*   lane-level rejection rounds */
     double chunk;                 /* samples per work item the launch used (rt_render_params.chunk or its default) */
+    double batches;               /* megakernel launches (sample batches) the job took */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */
@@ -216,11 +231,60 @@ int rt_device_free(void *ptr);
 int rt_copy_to_host(void *dst, const void *src_dev, uint64_t bytes);
 int rt_device_count(int *out);
 
+/* ------------------------------------------------ multi-GPU
+ * One process per GPU.  The root calls rt_dist_unique_id and hands the 128 bytes to
+ * every rank (any side channel); each rank calls rt_dist_init (ncclCommInitRank),
+ * renders its share of the pixels — the interleave of rt_rank_pixels: with
+ * world = a x b, rank (ry, rx) renders x = rx (mod a), y = ry (mod b), a sub-sampled
+ * copy of the whole view — and ONE ncclGather (rccl.h:745) brings the packed shares
+ * to the root, which unpacks them.  The RNG is keyed by (pixel, sample), so the
+ * image is bitwise the 1-GPU image for any rank count.                           */
+#define RT_DIST_ID_BYTES 128
+typedef struct rt_dist rt_dist;   /* one rank's RCCL communicator */
+int rt_dist_unique_id(uint8_t id[RT_DIST_ID_BYTES]);             /* ncclGetUniqueId (root only) */
+int rt_dist_init(const uint8_t id[RT_DIST_ID_BYTES], int rank, int world, int device, rt_dist **out);
+void rt_dist_destroy(rt_dist *d);
+/* ncclGather of `count` floats from every rank's send_dev into recv_dev on `root`
+ * (world x count floats, rank-major); enqueued on `stream` (hipStream_t, NULL = default). */
+int rt_dist_gather(rt_dist *d, const float *send_dev, uint64_t count, float *recv_dev, int root, void *stream);
+/* world = a x b, a >= b, as square as possible (8 -> 4 x 2). */
+void rt_interleave_factors(int world, int *a, int *b);
+/* The pixels of `rank` as 1x1 tiles (4 int32 each) in claim order: bands of 8 rows of
+ * the rank's lattice, column by column.  Returns the count (tiles == NULL: count only). */
+int64_t rt_rank_pixels(int nx, int ny, int rank, int world, int32_t *tiles, int64_t cap);
+/* Scatters packed tiles (rt_render_tiles' output layout) into an nx x ny x 3 image. */
+int rt_unpack_tiles(const float *packed, const int32_t *tiles, int64_t ntiles, int nx, int ny, float *image);
+/* The whole rank job: this rank's pixels -> rt_render_tiles -> rt_dist_gather -> on the
+ * root, the full nx x ny x 3 mean image in host memory (`image`; NULL on other ranks). */
+int rt_dist_render(rt_dist *d, rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p, float *image,
+                   rt_stats *stats);
+
 /* ----------------------------------------------------- resolve (main.cpp:314-330) */
 /* sqrt gamma + int(255.99*c) + clamp to 255, per channel (main.cpp:316-325). */
 void rt_quantize(const float *mean_rgb, int64_t n_pixels, uint8_t *rgb);
 /* P3 text of main.cpp:297,327-330; returns the byte count (writes when buf != NULL and cap suffices). */
 int64_t rt_ppm_text(const uint8_t *rgb, int nx, int ny, char *buf, int64_t cap);
+
+/* ------------------------------------------- checkpoint / resume
+ * A progressive render keeps per-pixel SUMS (RT_FLAG_SUM_OUT) and resumes from them
+ * (RT_FLAG_SUM_IN with sample_offset = samples_done): bitwise the same image as an
+ * uninterrupted render.  The file holds this header, `count` floats in the packed
+ * tile layout of rt_render_tiles, and a checksum; it is replaced atomically.       */
+#define RT_CHECKPOINT_MAGIC 0x4B435452u   /* "RTCK" */
+#define RT_CHECKPOINT_VERSION 1u
+typedef struct rt_checkpoint {
+    uint32_t magic, version;      /* set by rt_checkpoint_write */
+    int32_t nx, ny;               /* full image */
+    uint32_t samples_done;        /* the sums hold samples [0, samples_done) of every pixel */
+    int32_t max_depth, background;
+    float t_min;
+    uint64_t seed;                /* counter-RNG key of the render */
+    uint64_t job_hash;            /* caller's identification of the scene / tiles */
+    uint64_t count;               /* floats that follow (3 per pixel) */
+} rt_checkpoint;
+int rt_checkpoint_write(const char *path, const rt_checkpoint *hdr, const float *sums);
+/* sums == NULL reads the header only; otherwise cap = capacity of sums in floats. */
+int rt_checkpoint_read(const char *path, rt_checkpoint *hdr, float *sums, uint64_t cap);
 
 /* ------------------------------------------------ host scene construction */
 /* Builds one of the reference's scenes with the host API (random_scene, random_motion,

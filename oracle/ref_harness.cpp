@@ -105,6 +105,54 @@ static void tag_media(hitable **slot, int &next) {
     if (auto *n = dynamic_cast<bvh_node *>(h)) { tag_media(&n->left, next); if (n->right != n->left) tag_media(&n->right, next); return; }
 }
 
+// --------------------------------------------- corrected BVH (CPU baseline only)
+// The reference's bvh_node (bvh.h:29-54 hit, bvh.h:97-121 ctor: random axis, qsort by
+// box.min with the reference's own comparators bvh.h:58-95, split n/2) with ONE
+// change: the slab test uses the ray origin where aabb::hit (aabb.h:38-39) subtracts
+// the direction.  With the bug the reference's BVH misses hits, which is why the
+// shipped main renders final() as a flat list (main.cpp:291); this class gives the
+// "reference with a corrected BVH" throughput figure of BASELINE.md (--accel bvh).
+// Its ties go right (bvh.h:37-40), so images differ from the flat list in rare ties:
+// it is a timing baseline, never a parity oracle.
+static bool fixed_slab_hit(const aabb &b, const ray &r, float tmin, float tmax) {
+    for (int a = 0; a < 3; a++) {   // aabb.h:33-49 with origin()
+        float invD = 1.0f / r.direction()[a];
+        float t0 = (b.min()[a] - r.origin()[a]) * invD;
+        float t1 = (b.max()[a] - r.origin()[a]) * invD;
+        if (invD < 0.0f) std::swap(t0, t1);
+        tmin = t0 > tmin ? t0 : tmin;
+        tmax = t1 < tmax ? t1 : tmax;
+        if (tmax <= tmin) return false;
+    }
+    return true;
+}
+class fixed_bvh : public hitable {
+public:
+    fixed_bvh(hitable **l, int n, float time0, float time1) {
+        int axis = int(3 * drand48());
+        qsort(l, n, sizeof(hitable *), axis == 0 ? box_x_compare : (axis == 1 ? box_y_compare : box_z_compare));
+        if (n == 1) left = right = l[0];
+        else if (n == 2) { left = l[0]; right = l[1]; }
+        else { left = new fixed_bvh(l, n / 2, time0, time1); right = new fixed_bvh(l + n / 2, n - n / 2, time0, time1); }
+        aabb bl, br;
+        left->bounding_box(time0, time1, bl);
+        right->bounding_box(time0, time1, br);
+        box = surrounding_box(bl, br);
+    }
+    virtual bool hit(const ray &r, float tmin, float tmax, hit_record &rec) const {
+        if (!fixed_slab_hit(box, r, tmin, tmax)) return false;
+        hit_record lr, rr;
+        bool hl = left->hit(r, tmin, tmax, lr), hr = right->hit(r, tmin, tmax, rr);
+        if (hl && hr) { rec = lr.t < rr.t ? lr : rr; return true; }
+        if (hl) { rec = lr; return true; }
+        if (hr) { rec = rr; return true; }
+        return false;
+    }
+    virtual bool bounding_box(float, float, aabb &b) const { b = box; return true; }
+    hitable *left, *right;
+    aabb box;
+};
+
 // ------------------------------------------------------------ extra scenes
 // c3: the Chapter-1 motion-blur random scene (TNW/Chapter01:36-67) expressed with
 // the main.cpp texture API (checker ground main.cpp:54-57, constant textures).
@@ -263,14 +311,14 @@ static void usage() {
     fprintf(stderr,
         "ref_render --scene NAME [--nx N --ny N --ns N --depth D --bg black|sky --tmin T]\n"
         "           [--cam cornell|random|final_alt] [--rng canonical|counter --seed S]\n"
-        "           [--rows J0:J1] [--ppm FILE] [--fb FILE] [--dump FILE] [--perlin FILE] [--time]\n"
+        "           [--rows J0:J1] [--ppm FILE] [--fb FILE] [--dump FILE] [--perlin FILE] [--time] [--accel flat|bvh]\n"
         "  scenes: random_scene random_motion cornell_box cornell_smoke final simple_light two_spheres test\n"
         "          edge_empty edge_single edge_degenerate (sky, random camera)\n");
     exit(2);
 }
 
 int main(int argc, char **argv) {
-    std::string scene = "final", cam_name = "", bg = "", rng = "canonical", ppm, fb, dump, perlin_out, assets;
+    std::string scene = "final", cam_name = "", bg = "", rng = "canonical", ppm, fb, dump, perlin_out, assets, accel = "flat";
     int nx = 40, ny = 40, ns = 4, depth = -1, j_lo = 0, j_hi = -1; bool timing = false;
     double tmin = 0.001; uint64_t seed = 0;
     for (int a = 1; a < argc; a++) {
@@ -293,6 +341,7 @@ int main(int argc, char **argv) {
         else if (k == "--perlin") perlin_out = val();
         else if (k == "--time") timing = true;
         else if (k == "--assets") assets = val();
+        else if (k == "--accel") accel = val();
         else usage();
     }
     if (j_hi < 0) j_hi = ny;
@@ -334,6 +383,15 @@ int main(int argc, char **argv) {
         dump_node(world, "");
         fclose(g_dump);
     }
+
+    if (accel == "bvh") {   // corrected BVH over the world's list (timing baseline only)
+        auto *hl = dynamic_cast<hitable_list *>(world);
+        if (!hl || rng != "canonical") usage();
+        unsigned short saved_state[3];
+        memcpy(saved_state, g_canon_state, sizeof saved_state);   // the samples keep their draws
+        if (hl->list_size > 0) world = new fixed_bvh(hl->list, hl->list_size, 0.0f, 1.0f);
+        memcpy(g_canon_state, saved_state, sizeof saved_state);
+    } else if (accel != "flat") usage();
 
     if (bg.empty()) bg = sky_default ? "sky" : "black";
     if (depth < 0) depth = depth_default;

@@ -1,5 +1,4 @@
-// rt_device.h — device code shared by the two path-tracing engines (rt_kernel.hip:
-// the megakernel; rt_wavefront.hip: the workgroup wavefront): vectors, the counter
+// rt_device.h — device code of the path-tracing megakernel (rt_kernel.hip): vectors, the counter
 // RNG, primitive tests and hit records (the reference's hitable classes), textures
 // and Perlin noise, the BVH node step, and the wave-cooperative samplers.
 // Arithmetic follows the reference's float/double promotions; compiled with

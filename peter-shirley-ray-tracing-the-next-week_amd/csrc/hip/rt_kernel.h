@@ -5,7 +5,6 @@
 #include <stdint.h>
 
 #define RT_BLOCK 256      // 4 waves per workgroup
-#define RT_WF_SLOTS 1024  // path slots per workgroup of the wavefront engine
 
 // scene features a megakernel variant carries code for (rt_launch_megakernel)
 #define RT_FEAT_INST 1      // translate / rotate_y / flip_normals chains
@@ -39,31 +38,27 @@ struct RtKernelArgs {
     int nx, ny, ns, max_depth;
     float tmin;
     int background;
-    int chunk, nchunks;
-    uint32_t sample_offset;
+    int chunk, nchunks;       // samples per work item; work items per pixel in this launch
+    uint32_t sample_offset;   // sample index of this launch's first sample (batches: + batch start)
     uint64_t seed;
     // job: pixel list and outputs
     const uint32_t *job_xy;   // x | y << 16 per job pixel (image coords)
     uint32_t npix;
     uint32_t nitems;          // npix * nchunks
     uint32_t claim;           // work items per wave-level claim (a multiple of 64)
-    float4 *slab;             // [nchunks][npix] partial sums
+    float4 *slab;             // [nchunks][npix] partial sums of this launch's sample batch
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)
-    // wavefront engine path state (rt_wavefront.hip), grid x RT_WF_SLOTS records each
-    float4 *wf_ray_o;   // origin, time
-    float4 *wf_ray_d;   // direction, -
-    float2 *wf_hit;     // closest t, primitive (bits; ~0 none)
-    float4 *wf_beta;    // throughput, depth (int bits)
-    float4 *wf_part;    // the work item's running sum
-    uint4 *wf_rng;      // sample stream counter, medium key
-    uint4 *wf_samp;     // work item, next sample, end sample, -
 };
 
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);
-extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k,
+// Resolve of one sample batch (capi.cpp): adds the batch's partial sums to each
+// pixel's running sum in sample order.  mode: RT_RESOLVE_* bits.
+#define RT_RESOLVE_FIRST 1    // the first batch: start from 0 (or, with SUM_IN, from out)
+#define RT_RESOLVE_LAST 2     // the last batch: write out (times k unless RAW), else keep acc
+#define RT_RESOLVE_SUM_IN 4   // out holds the running sums of earlier samples on entry
+#define RT_RESOLVE_RAW 8      // write the sums themselves (checkpoints), not sum * k
+extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
-extern "C" hipError_t rt_launch_wavefront(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);
-extern "C" hipError_t rt_wavefront_occupancy(int *blocks_per_cu, int mode, int width);
 // mode: 0 plain, 1 count, 2 profile; width: BVH width of the scene (2 or 4)
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);

@@ -322,22 +322,37 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
     }
 }
 
-// Sums each pixel's chunk partials in chunk order and applies `col /= float(ns)`
-// (vec3.h:134-141: multiply by float(1.0/ns)).
+// Adds one sample batch's partial sums to each pixel's running sum, in sample
+// order (main.cpp:311 `col += temp`, one add per sample with one sample per work
+// item), so the image does not depend on how the samples were split into batches
+// (capi.cpp bounds the slab per launch).  The last batch applies `col /= float(ns)`
+// as the reciprocal multiply of vec3.h:134-141.
 __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ slab, uint32_t npix, int nchunks, float k,
+                                                  float4 *__restrict__ acc, int mode,
                                                   const uint32_t *__restrict__ out_index, float *__restrict__ out) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
+    const uint32_t o = out_index[p];
     V3 col = mk(0, 0, 0);
+    if (!(mode & RT_RESOLVE_FIRST)) {
+        const float4 a = acc[p];
+        col = mk(a.x, a.y, a.z);
+    } else if (mode & RT_RESOLVE_SUM_IN) {
+        col = mk(out[3 * (size_t)o + 0], out[3 * (size_t)o + 1], out[3 * (size_t)o + 2]);
+    }
 #pragma unroll 8
-    for (int c = 0; c < nchunks; ++c) {   // the loads run ahead; the adds stay in chunk order
+    for (int c = 0; c < nchunks; ++c) {   // the loads run ahead; the adds stay in sample order
         float4 v = slab[(size_t)c * npix + p];
         col = add(col, mk(v.x, v.y, v.z));
     }
-    uint32_t o = out_index[p];
-    out[3 * (size_t)o + 0] = col.x * k;
-    out[3 * (size_t)o + 1] = col.y * k;
-    out[3 * (size_t)o + 2] = col.z * k;
+    if (!(mode & RT_RESOLVE_LAST)) {
+        acc[p] = make_float4(col.x, col.y, col.z, 0.f);
+        return;
+    }
+    if (!(mode & RT_RESOLVE_RAW)) col = scale(k, col);
+    out[3 * (size_t)o + 0] = col.x;
+    out[3 * (size_t)o + 1] = col.y;
+    out[3 * (size_t)o + 2] = col.z;
 }
 
 }  // namespace
@@ -367,10 +382,10 @@ extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int 
     }
 }
 
-extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, const uint32_t *out_index,
-                                        float *out, hipStream_t stream) {
+extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
+                                        const uint32_t *out_index, float *out, hipStream_t stream) {
     int blocks = (int)((npix + 255) / 256);
-    hipLaunchKernelGGL(rt_resolve, dim3(blocks), dim3(256), 0, stream, slab, npix, nchunks, k, out_index, out);
+    hipLaunchKernelGGL(rt_resolve, dim3(blocks), dim3(256), 0, stream, slab, npix, nchunks, k, acc, mode, out_index, out);
     return hipGetLastError();
 }
 

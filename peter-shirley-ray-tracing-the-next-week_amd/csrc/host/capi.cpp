@@ -70,20 +70,18 @@ int commit(Arena &a, void **base) {
     return RT_OK;
 }
 
-// Resident workgroups per CU of the megakernel and the wavefront engine, per launch
-// mode and BVH width: a property of the code objects, queried once per process.
-hipError_t occupancy(int *mega, int *wave, int mode, int width) {
+// Resident workgroups per CU of the megakernel, per launch mode and BVH width: a
+// property of the code objects, queried once per process.
+hipError_t occupancy(int *mega, int mode, int width) {
     static std::mutex mu;
-    static int cache[3][2][2] = {};
+    static int cache[3][2] = {};
     std::lock_guard<std::mutex> lock(mu);
-    int *c = cache[mode][width == 4 ? 1 : 0];
-    if (!c[0]) {
+    int &c = cache[mode][width == 4 ? 1 : 0];
+    if (!c) {
         hipError_t e;
-        if ((e = rt_megakernel_occupancy(&c[0], mode, width)) != hipSuccess) return e;
-        if ((e = rt_wavefront_occupancy(&c[1], mode, width)) != hipSuccess) { c[0] = 0; return e; }
+        if ((e = rt_megakernel_occupancy(&c, mode, width)) != hipSuccess) { c = 0; return e; }
     }
-    *mega = c[0];
-    *wave = c[1];
+    *mega = c;
     return hipSuccess;
 }
 
@@ -132,11 +130,13 @@ double algorithmic_bytes(const rt_stats &st, double items, int bvh_width) {
 
 }  // namespace
 
+// shared with dist.cpp: sets the thread-local message rt_last_error() returns
+int rt_internal_fail(int code, const std::string &msg) { return fail(code, msg); }
+
 struct rt_scene {
     int device = 0;
     int cus = 0;
     int grid[3] = {0, 0, 0};      // persistent megakernel grid per variant (plain, count, profile)
-    int grid_wf[3] = {0, 0, 0};   // persistent wavefront-engine grid per variant
     hipStream_t own_stream = nullptr;
     // scene in HBM: one allocation (arena) holding the arrays below
     void *arena = nullptr;
@@ -155,9 +155,9 @@ struct rt_scene {
     void *job_xy = nullptr, *job_out = nullptr;
     void *slab = nullptr;
     size_t slab_bytes = 0;
+    void *acc = nullptr;          // per-pixel running sums between sample batches
+    size_t acc_bytes = 0;
     void *counter = nullptr, *stats = nullptr;
-    void *wf = nullptr;           // wavefront-engine path state (grid x RT_WF_SLOTS records)
-    size_t wf_bytes = 0;
     void *host_out = nullptr;
     size_t host_out_bytes = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -272,7 +272,7 @@ static int validate_desc(const rt_scene_desc *d) {
 void rt_scene_destroy(rt_scene *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
-    for (void *p : {s->wf, s->arena, s->job_xy, s->job_out, s->slab, s->counter, s->host_out})
+    for (void *p : {s->arena, s->job_xy, s->job_out, s->slab, s->acc, s->counter, s->host_out})
         if (p) (void)hipFree(p);
     for (auto &e : s->ev) if (e) (void)hipEventDestroy(e);
     if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
@@ -424,15 +424,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     if ((e = hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return cleanup(hip_fail(e, "hipDeviceGetAttribute"));
     for (int mode = 0; mode < 3; mode++) {
-        int bpc = 0, wbpc = 0;
-        if ((e = occupancy(&bpc, &wbpc, mode, s->bvh_width)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+        int bpc = 0;
+        if ((e = occupancy(&bpc, mode, s->bvh_width)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
         // RTNW_BLOCKS_PER_CU caps the resident workgroups per CU (occupancy experiments only)
-        if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) {
-            bpc = std::min(bpc, std::max(1, std::atoi(e)));
-            wbpc = std::min(wbpc, std::max(1, std::atoi(e)));
-        }
+        if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) bpc = std::min(bpc, std::max(1, std::atoi(e)));
         s->grid[mode] = std::max(1, bpc) * s->cus;
-        s->grid_wf[mode] = std::max(1, wbpc) * s->cus;
     }
     trace("device attributes");
     // the work counter (64 B) and the statistics counters in one allocation
@@ -449,10 +445,18 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     return RT_OK;
 }
 
-// Partial-sum slab budget of the default chunk choice (bytes).
+// Partial-sum slab budget per launch (bytes; env RTNW_SLAB_BUDGET overrides, for tests).
+// A job whose slab would be larger runs as several launches over sample batches.
 #ifndef RT_SLAB_BUDGET
 #define RT_SLAB_BUDGET (8ull << 30)
 #endif
+static uint64_t slab_budget() {
+    if (const char *e = std::getenv("RTNW_SLAB_BUDGET")) {
+        const unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v > 0) return v;
+    }
+    return RT_SLAB_BUDGET;
+}
 
 // Job pixel order: tiles in the order given; inside a tile, bands of 8 rows listed
 // column by column (8 pixels per column), so that ANY 64 consecutive items — a wave
@@ -500,23 +504,24 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     hipStream_t stream = (hipStream_t)stream_v;
     if (int rc = prepare_job(s, tiles, ntiles, p->nx, p->ny)) return rc;
 
-    // Default chunk: one sample per work item, unless the partial-sum slab would pass
-    // RT_SLAB_BUDGET or the item count 2^32; then the smallest chunk that fits.
-    // Short items keep each wave's lanes on neighbouring pixels (a wave deals its
-    // 64-item claims to lanes as they free up; long items let its pixels drift
-    // apart): 16 -> 1 sample per item is 92.2 -> 81.8 ms on c4.
-    int chunk = p->chunk;
-    if (chunk <= 0) {
-        chunk = 1;
-        while (chunk < p->spp &&
-               ((uint64_t)s->npix * (uint64_t)((p->spp + chunk - 1) / chunk) * 16 > RT_SLAB_BUDGET ||
-                (uint64_t)s->npix * (uint64_t)((p->spp + chunk - 1) / chunk) + 64 >= 0xFFFFFFFFull))
-            chunk *= 2;
-    }
-    const int nchunks = (p->spp + chunk - 1) / chunk;
-    const uint64_t nitems = (uint64_t)s->npix * (uint64_t)nchunks;
-    if (nitems + 64 >= 0xFFFFFFFFull) return fail(RT_ERR_INVALID, "job too large for one launch (pixels x chunks >= 2^32)");
-    const size_t slab_bytes = (size_t)nitems * 16;
+    // Work item = `chunk` samples of one pixel, one by default: short items keep each
+    // wave's lanes on neighbouring pixels (a wave deals its claims to lanes as they free
+    // up; long items let its pixels drift apart): 16 -> 1 sample per item is 92.2 ->
+    // 81.8 ms on c4.  The partial-sum slab holds one float4 per item
+    // of a launch; a job whose slab would pass the budget runs as several launches
+    // over sample batches (whole chunks), and the resolve adds every batch to a
+    // per-pixel running sum in sample order — so the sum is the same sequence of
+    // float adds whatever the batch size, i.e. the image does not depend on the job's
+    // size (one GPU or a rank's share of eight).
+    const int chunk = p->chunk > 0 ? p->chunk : 1;
+    const uint64_t nchunks_total = ((uint64_t)p->spp + chunk - 1) / chunk;
+    const uint64_t max_items = 0xFFFFFFFFull - 64;
+    if ((uint64_t)s->npix > max_items) return fail(RT_ERR_INVALID, "job too large (pixels >= 2^32)");
+    uint64_t per = std::max<uint64_t>(1, slab_budget() / ((uint64_t)s->npix * 16));
+    per = std::min<uint64_t>(per, max_items / s->npix);
+    per = std::min<uint64_t>(per, nchunks_total);
+    const uint64_t nbatches = (nchunks_total + per - 1) / per;
+    const size_t slab_bytes = (size_t)s->npix * per * 16;
     if (slab_bytes > s->slab_bytes) {
         if (s->slab) (void)hipFree(s->slab);
         s->slab = nullptr;
@@ -524,10 +529,18 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         HIP_TRY(hipMalloc(&s->slab, slab_bytes));
         s->slab_bytes = slab_bytes;
     }
+    const size_t acc_bytes = nbatches > 1 ? (size_t)s->npix * 16 : 0;
+    if (acc_bytes > s->acc_bytes) {
+        if (s->acc) (void)hipFree(s->acc);
+        s->acc = nullptr;
+        s->acc_bytes = 0;
+        HIP_TRY(hipMalloc(&s->acc, acc_bytes));
+        s->acc_bytes = acc_bytes;
+    }
     const bool count = (p->flags & RT_FLAG_COUNT) != 0;
     const bool prof = !count && (p->flags & RT_FLAG_PROFILE) != 0;
+    const bool sum_in = (p->flags & RT_FLAG_SUM_IN) != 0, sum_out = (p->flags & RT_FLAG_SUM_OUT) != 0;
     const int mode = count ? 1 : (prof ? 2 : 0);
-    HIP_TRY(hipMemsetAsync(s->counter, 0, 64, stream));
     if (count || prof) HIP_TRY(hipMemsetAsync(s->stats, 0, (RT_CNT_N + 16) * sizeof(unsigned long long), stream));
 
     RtKernelArgs a{};
@@ -567,67 +580,60 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.tmin = p->t_min;
     a.background = p->background;
     a.chunk = chunk;
-    a.nchunks = nchunks;
-    a.sample_offset = p->sample_offset;
     a.seed = p->seed;
     a.job_xy = (const uint32_t *)s->job_xy;
     a.npix = s->npix;
-    a.nitems = (uint32_t)nitems;
     a.slab = (float4 *)s->slab;
     a.counter = (uint32_t *)s->counter;
     a.stats = (unsigned long long *)s->stats;
 
-    // engine: the megakernel (default) or the workgroup wavefront (RTNW_ENGINE=wave,
-    // rt_wavefront.hip)
-    const char *eng = std::getenv("RTNW_ENGINE");
-    const bool wave = eng && std::strcmp(eng, "wave") == 0;
-    // Claim size: up to 512 items per atomic (64 -> 512 is 81.6 -> 76.9 ms on c4: fewer
-    // round trips to the one contended counter), at least 8 claims per
-    // wave so that small jobs still spread over every wave.
-    {
-        const uint64_t waves = (uint64_t)(wave ? s->grid_wf[mode] : s->grid[mode]) * (RT_BLOCK / 64);
-        uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nitems / (waves * 8) / 64 * 64, 64), 512);
-        if (const char *e = std::getenv("RTNW_CLAIM")) c = (uint64_t)std::max(1, std::atoi(e)) * 64;   // x 64 items
-        a.claim = (uint32_t)c;
-    }
-    if (wave) {
-        const size_t nslots = (size_t)s->grid_wf[mode] * RT_WF_SLOTS;
-        const size_t need = nslots * (5 * sizeof(float4) + sizeof(float2) + sizeof(uint4));
-        if (need > s->wf_bytes) {
-            if (s->wf) (void)hipFree(s->wf);
-            s->wf = nullptr;
-            s->wf_bytes = 0;
-            HIP_TRY(hipMalloc(&s->wf, need));
-            s->wf_bytes = need;
+    // vec3::operator/= (vec3.h:134-141): col *= float(1.0 / ns)
+    const uint32_t ns_total = sum_in ? p->sample_offset + (uint32_t)p->spp : (uint32_t)p->spp;
+    const float k = (float)(1.0 / (double)(float)ns_total);
+    const uint64_t waves = (uint64_t)s->grid[mode] * (RT_BLOCK / 64);
+    double kernel_ms = 0, resolve_ms = 0;
+    for (uint64_t b = 0; b < nbatches; ++b) {
+        const uint64_t c0 = b * per, c1 = std::min(c0 + per, nchunks_total);
+        const uint64_t s0 = c0 * (uint64_t)chunk, s1 = std::min<uint64_t>(c1 * (uint64_t)chunk, (uint64_t)p->spp);
+        a.ns = (int)(s1 - s0);                                   // samples of this batch
+        a.sample_offset = p->sample_offset + (uint32_t)s0;       // their first sample index
+        a.nchunks = (int)(c1 - c0);
+        const uint64_t nitems = (uint64_t)s->npix * (c1 - c0);
+        a.nitems = (uint32_t)nitems;
+        // Claim size: up to 512 items per atomic (64 -> 512 is 81.6 -> 76.9 ms on c4:
+        // fewer round trips to the one contended counter), at least 8
+        // claims per wave so that small jobs still spread over every wave.
+        {
+            uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nitems / (waves * 8) / 64 * 64, 64), 512);
+            if (const char *e = std::getenv("RTNW_CLAIM")) c = (uint64_t)std::max(1, std::atoi(e)) * 64;   // x 64 items
+            a.claim = (uint32_t)c;
         }
-        char *w = (char *)s->wf;
-        a.wf_ray_o = (float4 *)w; w += nslots * sizeof(float4);
-        a.wf_ray_d = (float4 *)w; w += nslots * sizeof(float4);
-        a.wf_beta = (float4 *)w; w += nslots * sizeof(float4);
-        a.wf_part = (float4 *)w; w += nslots * sizeof(float4);
-        a.wf_rng = (uint4 *)w; w += nslots * sizeof(uint4);
-        a.wf_samp = (uint4 *)w; w += nslots * sizeof(uint4);
-        a.wf_hit = (float2 *)w;
+        const int rmode = (b == 0 ? RT_RESOLVE_FIRST : 0) | (b + 1 == nbatches ? RT_RESOLVE_LAST : 0) |
+                          (sum_in ? RT_RESOLVE_SUM_IN : 0) | (sum_out ? RT_RESOLVE_RAW : 0);
+        HIP_TRY(hipMemsetAsync(s->counter, 0, 64, stream));
+        HIP_TRY(hipEventRecord(s->ev[0], stream));
+        HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
+        HIP_TRY(hipEventRecord(s->ev[1], stream));
+        HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, a.nchunks, k, (float4 *)s->acc, rmode,
+                                  (const uint32_t *)s->job_out, out_dev, stream));
+        HIP_TRY(hipEventRecord(s->ev[2], stream));
+        if (stats) {   // one batch at a time: the events are reused
+            HIP_TRY(hipEventSynchronize(s->ev[2]));
+            float ms0 = 0, ms1 = 0;
+            HIP_TRY(hipEventElapsedTime(&ms0, s->ev[0], s->ev[1]));
+            HIP_TRY(hipEventElapsedTime(&ms1, s->ev[1], s->ev[2]));
+            kernel_ms += ms0;
+            resolve_ms += ms1;
+        }
     }
-
-    const float k = (float)(1.0 / (double)(float)p->spp);   // vec3::operator/= (vec3.h:134-141)
-    HIP_TRY(hipEventRecord(s->ev[0], stream));
-    if (wave) HIP_TRY(rt_launch_wavefront(&a, s->grid_wf[mode], mode, stream));
-    else HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
-    HIP_TRY(hipEventRecord(s->ev[1], stream));
-    HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, nchunks, k, (const uint32_t *)s->job_out, out_dev, stream));
-    HIP_TRY(hipEventRecord(s->ev[2], stream));
 
     if (stats) {
-        HIP_TRY(hipEventSynchronize(s->ev[2]));
-        float ms0 = 0, ms1 = 0;
-        HIP_TRY(hipEventElapsedTime(&ms0, s->ev[0], s->ev[1]));
-        HIP_TRY(hipEventElapsedTime(&ms1, s->ev[1], s->ev[2]));
         std::memset(stats, 0, sizeof *stats);
         stats->samples = (double)s->npix * (double)p->spp;
         stats->chunk = (double)chunk;
-        stats->kernel_ms = ms0;
-        stats->resolve_ms = ms1;
+        stats->batches = (double)nbatches;
+        stats->kernel_ms = kernel_ms;
+        stats->resolve_ms = resolve_ms;
         if (count) {
             unsigned long long c[RT_CNT_N];
             HIP_TRY(hipMemcpy(c, s->stats, sizeof c, hipMemcpyDeviceToHost));
@@ -641,7 +647,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->medium_tests = (double)c[RT_CNT_MEDIA];
             stats->shades = (double)c[RT_CNT_SHADES];
             stats->noise_evals = (double)c[RT_CNT_NOISE];
-            stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)nitems, s->bvh_width);
+            stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)s->npix * (double)nchunks_total, s->bvh_width);
             unsigned long long w[5];
             HIP_TRY(hipMemcpy(w, (unsigned long long *)s->stats + RT_CNT_N + 4, sizeof w, hipMemcpyDeviceToHost));
             stats->wave_iterations = (double)w[0];
@@ -658,7 +664,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->cycles_media = (double)c[RT_CNT_N + 2];
             stats->cycles_shade = (double)c[RT_CNT_N + 3];
         }
-        stats->grid = (double)(wave ? s->grid_wf[mode] : s->grid[mode]);
+        stats->grid = (double)s->grid[mode];
     }
     return RT_OK;
 }
@@ -678,6 +684,8 @@ int rt_render_tile(rt_scene *s, const rt_camera_desc *cam, const rt_render_param
     }
     if (!s->own_stream) HIP_TRY(hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking));
     const int32_t tile[4] = {x0, y0, w, h};
+    if (p && (p->flags & RT_FLAG_SUM_IN))   // the running sums come from the caller's buffer
+        HIP_TRY(hipMemcpyAsync(s->host_out, out_rgb, bytes, hipMemcpyHostToDevice, s->own_stream));
     rt_stats local;
     if (int rc = rt_render_tiles(s, cam, p, tile, 1, (float *)s->host_out, s->own_stream, stats ? stats : &local)) return rc;
     HIP_TRY(hipMemcpyAsync(out_rgb, s->host_out, bytes, hipMemcpyDeviceToHost, s->own_stream));
@@ -703,6 +711,63 @@ int64_t rt_ppm_text(const uint8_t *rgb, int nx, int ny, char *buf, int64_t cap) 
         s += std::to_string(rgb[3 * q]) + " " + std::to_string(rgb[3 * q + 1]) + " " + std::to_string(rgb[3 * q + 2]) + "\n";
     if (buf && cap >= (int64_t)s.size()) std::memcpy(buf, s.data(), s.size());
     return (int64_t)s.size();
+}
+
+// ------------------------------------------------ checkpoint / resume
+// File = rt_checkpoint header, `count` floats (the per-pixel sums as rt_render_tiles
+// packs them), FNV-1a 64 of those bytes.  Written to <path>.tmp, then renamed, so a
+// crash leaves either the previous checkpoint or the new one, never a torn file (the
+// reference's row-by-row PPM write, main.cpp:330, leaves a truncated image).
+static uint64_t fnv1a(const void *p, size_t n) {
+    const uint8_t *b = (const uint8_t *)p;
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < n; i++) { h ^= b[i]; h *= 0x100000001b3ull; }
+    return h;
+}
+
+int rt_checkpoint_write(const char *path, const rt_checkpoint *hdr, const float *sums) {
+    if (!path || !hdr || (!sums && hdr->count)) return fail(RT_ERR_INVALID, "rt_checkpoint_write: null argument");
+    rt_checkpoint h = *hdr;
+    h.magic = RT_CHECKPOINT_MAGIC;
+    h.version = RT_CHECKPOINT_VERSION;
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE *f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return fail(RT_ERR_INVALID, std::string("cannot open ") + tmp);
+    const size_t bytes = (size_t)h.count * sizeof(float);
+    const uint64_t sum = fnv1a(sums, bytes);
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && (bytes == 0 || std::fwrite(sums, 1, bytes, f) == bytes) &&
+              std::fwrite(&sum, sizeof sum, 1, f) == 1;
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path) != 0) {
+        std::remove(tmp.c_str());
+        return fail(RT_ERR_INVALID, std::string("cannot write checkpoint ") + path);
+    }
+    return RT_OK;
+}
+
+int rt_checkpoint_read(const char *path, rt_checkpoint *hdr, float *sums, uint64_t cap) {
+    if (!path || !hdr) return fail(RT_ERR_INVALID, "rt_checkpoint_read: null argument");
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return fail(RT_ERR_INVALID, std::string("cannot open ") + path);
+    rt_checkpoint h;
+    int rc = RT_OK;
+    if (std::fread(&h, sizeof h, 1, f) != 1 || h.magic != RT_CHECKPOINT_MAGIC || h.version != RT_CHECKPOINT_VERSION) {
+        rc = fail(RT_ERR_INVALID, std::string("not a checkpoint: ") + path);
+    } else if (sums) {   // sums == NULL: header only (to size the buffer)
+        if (h.count > cap) {
+            rc = fail(RT_ERR_INVALID, "checkpoint larger than the buffer");
+        } else {
+            const size_t bytes = (size_t)h.count * sizeof(float);
+            uint64_t sum = 0;
+            if ((bytes && std::fread(sums, 1, bytes, f) != bytes) || std::fread(&sum, sizeof sum, 1, f) != 1)
+                rc = fail(RT_ERR_INVALID, std::string("truncated checkpoint: ") + path);
+            else if (sum != fnv1a(sums, bytes))
+                rc = fail(RT_ERR_INVALID, std::string("checkpoint checksum mismatch: ") + path);
+        }
+    }
+    std::fclose(f);
+    if (rc == RT_OK) *hdr = h;
+    return rc;
 }
 
 // ------------------------------------------------------- host scene building

@@ -27,6 +27,9 @@ RT_OK = 0
 RT_BG_BLACK, RT_BG_SKY = 0, 1
 RT_FLAG_COUNT = 1
 RT_FLAG_PROFILE = 2
+RT_FLAG_SUM_IN = 4      # the output holds the sums of samples [0, sample_offset) on entry
+RT_FLAG_SUM_OUT = 8     # write per-pixel sums (checkpoints), not means
+RT_CHECKPOINT_MAGIC = 0x4B435452
 
 
 class RtError(RuntimeError):
@@ -89,10 +92,18 @@ class RtStats(ctypes.Structure):
         "samples", "segments", "node_visits", "sphere_tests", "moving_sphere_tests", "rect_tests", "instanced_tests",
         "medium_tests", "shades", "noise_evals", "algorithmic_bytes", "kernel_ms", "resolve_ms",
         "cycles_claim", "cycles_traverse", "cycles_media", "cycles_shade", "grid", "wave_iterations",
-        "wave_node_trips", "wave_prim_trips", "wave_sphere_draw_trips", "lane_sphere_draw_trips", "chunk")]
+        "wave_node_trips", "wave_prim_trips", "wave_sphere_draw_trips", "lane_sphere_draw_trips", "chunk",
+        "batches")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class RtCheckpoint(ctypes.Structure):
+    _fields_ = [("magic", ctypes.c_uint32), ("version", ctypes.c_uint32), ("nx", ctypes.c_int32),
+                ("ny", ctypes.c_int32), ("samples_done", ctypes.c_uint32), ("max_depth", ctypes.c_int32),
+                ("background", ctypes.c_int32), ("t_min", ctypes.c_float), ("seed", ctypes.c_uint64),
+                ("job_hash", ctypes.c_uint64), ("count", ctypes.c_uint64)]
 
 
 _lib = None
@@ -129,6 +140,20 @@ def lib():
             "rt_builtin_scene_desc": (ctypes.c_int, [ctypes.c_char_p, P(P(RtSceneDesc))]),
             "rt_scene_desc_free": (None, [P(RtSceneDesc)]),
             "rt_scene_desc_dump": (ctypes.c_int64, [P(RtSceneDesc), ctypes.c_char_p, ctypes.c_int64]),
+            "rt_checkpoint_write": (ctypes.c_int, [ctypes.c_char_p, P(RtCheckpoint), ctypes.c_void_p]),
+            "rt_checkpoint_read": (ctypes.c_int, [ctypes.c_char_p, P(RtCheckpoint), ctypes.c_void_p, ctypes.c_uint64]),
+            "rt_dist_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+            "rt_dist_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(ctypes.c_void_p)]),
+            "rt_dist_destroy": (None, [ctypes.c_void_p]),
+            "rt_dist_gather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                              ctypes.c_int, ctypes.c_void_p]),
+            "rt_interleave_factors": (None, [ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int)]),
+            "rt_rank_pixels": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_int64]),
+            "rt_unpack_tiles": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_void_p]),
+            "rt_dist_render": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, P(RtCameraDesc), P(RtRenderParams),
+                                              ctypes.c_void_p, P(RtStats)]),
             "rt_last_error": (ctypes.c_char_p, []),
             "rt_version": (ctypes.c_char_p, []),
         }
@@ -258,8 +283,15 @@ class Scene:
     def builtin(cls, name: str, device: int = 0, earth_png: str | None = None) -> "Scene":
         return cls(SceneDesc.builtin(name, earth_png), device)
 
-    def render_tile(self, cam: Camera, params: RtRenderParams, x0, y0, w, h, stats: bool = False):
+    def render_tile(self, cam: Camera, params: RtRenderParams, x0, y0, w, h, stats: bool = False, sums=None):
+        """Mean radiance of the w x h tile ([h, w, 3] float32).  With RT_FLAG_SUM_IN,
+        `sums` holds the running sums of samples [0, params.sample_offset) (e.g. from
+        read_checkpoint); with RT_FLAG_SUM_OUT the result is sums, not means."""
         out = np.zeros((h, w, 3), dtype=np.float32)
+        if params.flags & RT_FLAG_SUM_IN:
+            if sums is None:
+                raise ValueError("RT_FLAG_SUM_IN needs the running sums")
+            out[...] = np.asarray(sums, np.float32).reshape(h, w, 3)
         st = RtStats()
         _check(lib().rt_render_tile(self.handle, ctypes.byref(cam.desc), ctypes.byref(params), x0, y0, w, h,
                                     out.ctypes.data, ctypes.byref(st)))
@@ -284,6 +316,75 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+# ------------------------------------------------------------ multi-GPU (RCCL)
+RT_DIST_ID_BYTES = 128
+
+
+def dist_unique_id() -> bytes:
+    """ncclGetUniqueId (rt_dist_unique_id): created on the root, handed to every rank."""
+    buf = ctypes.create_string_buffer(RT_DIST_ID_BYTES)
+    _check(lib().rt_dist_unique_id(buf))
+    return buf.raw
+
+
+class Dist:
+    """One rank's RCCL communicator (rt_dist_init = ncclCommInitRank)."""
+
+    def __init__(self, uid: bytes, rank: int, world: int, device: int):
+        assert len(uid) == RT_DIST_ID_BYTES
+        self.rank, self.world = rank, world
+        self.handle = ctypes.c_void_p()
+        _check(lib().rt_dist_init(ctypes.create_string_buffer(uid, RT_DIST_ID_BYTES), rank, world, device,
+                                  ctypes.byref(self.handle)))
+
+    def gather(self, send_dev: int, count: int, recv_dev: int, root: int = 0, stream: int = 0):
+        """ncclGather (rccl.h:745) of `count` floats per rank to `root` (world x count floats)."""
+        _check(lib().rt_dist_gather(self.handle, ctypes.c_void_p(send_dev), count, ctypes.c_void_p(recv_dev), root,
+                                    ctypes.c_void_p(stream)))
+
+    def render(self, scene: "Scene", cam: "Camera", params: RtRenderParams):
+        """rt_dist_render: this rank's pixels -> render -> gather; the image on rank 0."""
+        img = np.zeros((params.ny, params.nx, 3), np.float32) if self.rank == 0 else None
+        st = RtStats()
+        _check(lib().rt_dist_render(self.handle, scene.handle, ctypes.byref(cam.desc), ctypes.byref(params),
+                                    img.ctypes.data if img is not None else None, ctypes.byref(st)))
+        return img, st.as_dict()
+
+    def close(self):
+        if self.handle:
+            lib().rt_dist_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+def rank_pixels_c(nx, ny, rank, world):
+    """The C ABI's pixel interleave (rt_rank_pixels); equals pixels_for_rank."""
+    n = lib().rt_rank_pixels(nx, ny, rank, world, None, 0)
+    _check(0 if n >= 0 else int(n))
+    t = np.zeros((n, 4), np.int32)
+    _check(0 if lib().rt_rank_pixels(nx, ny, rank, world, t.ctypes.data, n) == n else -1)
+    return t
+
+
+# ------------------------------------------------------- checkpoint / resume
+def write_checkpoint(path: str, sums: np.ndarray, *, nx, ny, samples_done, params: RtRenderParams | None = None,
+                     job_hash: int = 0):
+    """Persists per-pixel sums (rt_checkpoint_write: atomic replace, checksummed)."""
+    a = np.ascontiguousarray(sums, dtype=np.float32)
+    h = RtCheckpoint(nx=nx, ny=ny, samples_done=samples_done, job_hash=job_hash, count=a.size)
+    if params is not None:
+        h.max_depth, h.background, h.t_min, h.seed = params.max_depth, params.background, params.t_min, params.seed
+    _check(lib().rt_checkpoint_write(os.fsencode(path), ctypes.byref(h), a.ctypes.data))
+
+
+def read_checkpoint(path: str):
+    """Returns (header dict, float32 sums) of a checkpoint file."""
+    h = RtCheckpoint()
+    _check(lib().rt_checkpoint_read(os.fsencode(path), ctypes.byref(h), None, 0))
+    a = np.zeros(h.count, np.float32)
+    _check(lib().rt_checkpoint_read(os.fsencode(path), ctypes.byref(h), a.ctypes.data, a.size))
+    return {n: getattr(h, n) for n, _ in h._fields_}, a
 
 
 # -------------------------------------------------------------------- resolve

@@ -101,3 +101,80 @@ def test_interleave_claims_are_local():
         local = [np.ptp(g[:, 0]) < 8 * a and np.ptp(g[:, 1]) < 16 * b
                  for g in (t[k:k + 64] for k in range(0, len(t) - 64, 64))]
         assert np.mean(local) > 0.9, (world, np.mean(local))
+
+
+def _gpu_worker(rank, world, port, q):
+    """One rank of the product path: its interleaved pixels through librt_hip.so
+    (rt_render_tiles into device memory), gathered with gloo to rank 0."""
+    import ctypes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tiles = rtnw.pixels_for_rank(NX, NY, rank, world)
+    nmax = max(len(rtnw.pixels_for_rank(NX, NY, r, world)) for r in range(world)) * 3
+    sc = rtnw.Scene.builtin("final", device=0)
+    cam = rtnw.Camera.preset("cornell", NX, NY)
+    p = rtnw.RenderParams(NX, NY, NS, seed=SEED)
+    L = rtnw.lib()
+    dev = ctypes.c_void_p()
+    assert L.rt_device_alloc(0, nmax * 4, ctypes.byref(dev)) == 0
+    st = sc.render_tiles(cam, p, tiles, dev.value)
+    buf = np.zeros(nmax, np.float32)
+    assert L.rt_copy_to_host(buf.ctypes.data, dev, len(tiles) * 12) == 0
+    L.rt_device_free(dev)
+    t = torch.from_numpy(buf)
+    gl = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, gl, dst=0)
+    if rank == 0:
+        img = np.zeros((NY, NX, 3), np.float32)
+        for r in range(world):
+            tr = rtnw.pixels_for_rank(NX, NY, r, world)
+            rtnw.unpack_tiles(gl[r][: 3 * len(tr)].numpy(), tr, img)
+        q.put((img, st["samples"]))
+    dist.barrier()
+    sc.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gloo_gather_of_product_renders_equals_single_gpu_image():
+    """World size 2 on one GPU, each rank driving librt_hip.so (not the oracle): the
+    gathered image == the 1-rank GPU image bitwise == the oracle within the bar."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    img, samples = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert samples == len(rtnw.pixels_for_rank(NX, NY, 0, 2)) * NS
+    sc = rtnw.Scene.builtin("final", device=0)
+    one = sc.render_tile(rtnw.Camera.preset("cornell", NX, NY), rtnw.RenderParams(NX, NY, NS, seed=SEED), 0, 0, NX, NY)
+    assert np.array_equal(img.view(np.uint32), one.view(np.uint32))
+    ora, _ = O.render(O.kernel_spec("final", NX, NY, NS, seed=SEED, chunk=1))
+    g = np.sqrt(np.clip(img, 0, 1)) - np.sqrt(np.clip(ora, 0, 1))
+    assert (np.sqrt(np.mean(g ** 2, axis=(0, 1))) <= 1e-3).all()
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_communicator_gather_equals_render_tile():
+    """The native multi-GPU path (rt_dist_*: ncclGetUniqueId, ncclCommInitRank,
+    ncclGather) with a 1-rank communicator — the gather to self — returns exactly the
+    rt_render_tile image; then the raw gather of a device buffer to itself."""
+    nx, ny, ns = 64, 48, 6
+    sc = rtnw.Scene.builtin("final", device=0)
+    cam = rtnw.Camera.preset("cornell", nx, ny)
+    p = rtnw.RenderParams(nx, ny, ns, seed=3)
+    d = rtnw.Dist(rtnw.dist_unique_id(), 0, 1, 0)
+    img, st = d.render(sc, cam, p)
+    assert st["samples"] == nx * ny * ns
+    ref = sc.render_tile(cam, p, 0, 0, nx, ny)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    data = torch.arange(1000, dtype=torch.float32, device="cuda")
+    recv = torch.zeros(1000, dtype=torch.float32, device="cuda")
+    d.gather(data.data_ptr(), 1000, recv.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(recv, data)
+    d.close()

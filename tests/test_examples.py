@@ -41,3 +41,23 @@ def test_example_matches_python_path(scene):
     cam = rtnw.Camera.preset("cornell", 48, 40)
     mean = sc.render_tile(cam, rtnw.RenderParams(48, 40, 8, seed=1), 0, 0, 48, 40)
     assert open(out, "rb").read() == rtnw.ppm_text(rtnw.quantize(mean))
+
+
+def test_dist_example_compiles():
+    _build()
+    assert os.access(os.path.join(EX, "render_dist"), os.X_OK)
+
+
+@pytest.mark.gpu
+def test_dist_example_one_rank_matches_python_path():
+    """examples/render_dist (the RCCL driver, no PyTorch) with one rank per GPU of this
+    box: its PPM == the Python path's PPM with the same parameters."""
+    exe = os.path.join(EX, "render_dist")
+    _build()
+    out = os.path.join(tempfile.mkdtemp(), "d.ppm")
+    r = subprocess.run([exe, "--ranks", "1", "--nx", "40", "--ny", "32", "--ns", "8", "--seed", "5", "--ppm", out],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    sc = rtnw.Scene.builtin("final")
+    mean = sc.render_tile(rtnw.Camera.preset("cornell", 40, 32), rtnw.RenderParams(40, 32, 8, seed=5), 0, 0, 40, 32)
+    assert open(out, "rb").read() == rtnw.ppm_text(rtnw.quantize(mean))

@@ -233,17 +233,108 @@ def test_default_work_item_is_one_sample_in_reference_order():
     assert (gamma_rms(a, o) <= TOL_RMS).all()
 
 
-def test_large_job_doubles_the_chunk_and_keeps_parity():
-    """Past the 8 GiB partial-sum slab (16 B x pixels x samples per item) the default
-    work item holds 2 samples (capi.cpp): 1000 x 1000 x 600 spp = 600 M samples.
-    Checked on sampled crops against the oracle with the same chunk."""
-    nx, ny, ns = 1000, 1000, 600
-    g, st = gpu_render("cornell_box", nx, ny, ns, seed=31, chunk=0, stats=True)
-    assert st["chunk"] == 2
-    assert np.isfinite(g).all() and (g >= 0).all()
+def _render_shares(scene, nx, ny, ns, world, seed):
+    """final() etc. rendered as `world` interleaved rank shares (rtnw.pixels_for_rank,
+    as bench.py / the RCCL driver split config 5), each packed in device memory,
+    unpacked on the 'root': the image the multi-GPU gather assembles."""
+    import ctypes
+    cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene]
+    cam = rtnw.Camera.preset(cam_name, nx, ny)
+    p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, seed=seed)
+    sc = _scene(scene)
+    L = rtnw.lib()
+    img = np.zeros((ny, nx, 3), np.float32)
+    batches = []
+    for r in range(world):
+        tiles = rtnw.pixels_for_rank(nx, ny, r, world)
+        n = len(tiles) * 3
+        dev = ctypes.c_void_p()
+        assert L.rt_device_alloc(0, n * 4, ctypes.byref(dev)) == 0
+        st = sc.render_tiles(cam, p, tiles, dev.value)
+        batches.append(st["batches"])
+        packed = np.zeros(n, np.float32)
+        assert L.rt_copy_to_host(packed.ctypes.data, dev, n * 4) == 0
+        L.rt_device_free(dev)
+        rtnw.unpack_tiles(packed, tiles, img)
+    return img, batches
+
+
+def test_config5_image_is_independent_of_rank_count_and_batching(monkeypatch):
+    """Config 5 (final() 1000 x 1000, tiled over 8 GPUs) at reduced spp: the 1-GPU job
+    and the 8 interleaved rank shares must be bitwise equal although they split the
+    samples into different numbers of launches.  The slab budget is lowered
+    (RTNW_SLAB_BUDGET) so that the 1-GPU job takes 4 sample batches and each 1/8 share
+    one: each batch is added to the per-pixel running sum in sample order
+    (main.cpp:311), so the sums are the same float adds.  Oracle crops pin it."""
+    nx, ny, ns, seed = 1000, 1000, 8, 55
+    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(1000 * 1000 * 16 * 2))   # 2 samples per launch for 1e6 pixels
+    one, b1 = _render_shares("final", nx, ny, ns, 1, seed)
+    eight, b8 = _render_shares("final", nx, ny, ns, 8, seed)
+    assert b1 == [4.0] and set(b8) == {1.0}, (b1, b8)
+    monkeypatch.delenv("RTNW_SLAB_BUDGET")
+    default, bd = _render_shares("final", nx, ny, ns, 1, seed)
+    assert bd == [1.0]
+    assert np.array_equal(one.view(np.uint32), eight.view(np.uint32))
+    assert np.array_equal(one.view(np.uint32), default.view(np.uint32))
+    assert np.isfinite(one).all() and (one >= 0).all()
     for x0, y0 in ((0, 0), (496, 508), (992, 992)):
-        o = oracle_render("cornell_box", nx, ny, ns, seed=31, chunk=2, rect=(x0, y0, 8, 8))
-        assert (gamma_rms(g[y0:y0 + 8, x0:x0 + 8], o) <= TOL_RMS).all()
+        o = oracle_render("final", nx, ny, ns, seed=seed, chunk=1, rect=(x0, y0, 8, 8))
+        assert (gamma_rms(one[y0:y0 + 8, x0:x0 + 8], o) <= TOL_RMS).all()
+
+
+def test_batches_keep_explicit_chunks_whole(monkeypatch):
+    """An explicit chunk (samples per work item) with a budget that forces batches:
+    batches hold whole chunks, so the per-item partial sums and their order are the
+    same as in one launch."""
+    nx, ny, ns = 96, 64, 21
+    ref = gpu_render("cornell_box", nx, ny, ns, seed=12, chunk=4)
+    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(nx * ny * 16 * 2))   # 2 chunks (8 samples) per launch
+    img, st = gpu_render("cornell_box", nx, ny, ns, seed=12, chunk=4, stats=True)
+    assert st["batches"] == 3
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+
+
+def test_checkpoint_resume_is_bitwise_the_uninterrupted_render(tmp_path):
+    """Progressive render (SURVEY §5 checkpoint/resume): 5 samples as sums
+    (RT_FLAG_SUM_OUT) -> rt_checkpoint_write -> rt_checkpoint_read -> 7 more samples
+    added to them (RT_FLAG_SUM_IN, sample_offset 5) == the 12-sample render."""
+    nx, ny, ns = 48, 32, 12
+    cam = rtnw.Camera.preset("cornell", nx, ny)
+    sc = _scene("final")
+    full = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=77), 0, 0, nx, ny)
+    p1 = rtnw.RenderParams(nx, ny, 5, seed=77, flags=rtnw.RT_FLAG_SUM_OUT)
+    sums = sc.render_tile(cam, p1, 0, 0, nx, ny)
+    path = str(tmp_path / "final.rtck")
+    rtnw.write_checkpoint(path, sums, nx=nx, ny=ny, samples_done=5, params=p1, job_hash=1234)
+    hdr, back = rtnw.read_checkpoint(path)
+    assert hdr["samples_done"] == 5 and hdr["job_hash"] == 1234 and hdr["seed"] == 77
+    p2 = rtnw.RenderParams(nx, ny, ns - 5, seed=77, sample_offset=hdr["samples_done"], flags=rtnw.RT_FLAG_SUM_IN)
+    resumed = sc.render_tile(cam, p2, 0, 0, nx, ny, sums=back)
+    assert np.array_equal(resumed.view(np.uint32), full.view(np.uint32))
+    # the sums themselves: 5 samples' sum times float(1/5) is the 5-sample mean
+    mean5 = sc.render_tile(cam, rtnw.RenderParams(nx, ny, 5, seed=77), 0, 0, nx, ny)
+    assert np.array_equal((sums * np.float32(1.0 / 5)).view(np.uint32), mean5.view(np.uint32))
+
+
+@pytest.mark.parametrize("scene,nx,ny,ns", [("cornell_box", 400, 400, 200), ("random_motion", 800, 400, 500),
+                                            ("final", 500, 500, 1000)])
+def test_baseline_configs_at_full_spp_against_oracle_crops(scene, nx, ny, ns):
+    """BASELINE.json c2 / c3 / c4 exactly as bench.py renders them (full image, full
+    spp, default work items): four 8x8 crops recomputed by the oracle at the same spp
+    (main.cpp:299-316).  Reports the bit-exact fraction."""
+    g = gpu_render(scene, nx, ny, ns, seed=2024, chunk=0)
+    assert np.isfinite(g).all() and (g >= 0).all()
+    rng = np.random.default_rng(ns)
+    exact = []
+    for k in range(4):
+        x0 = int(rng.integers(0, nx - 8)) if k else nx // 2 - 4
+        y0 = int(rng.integers(0, ny - 8)) if k else ny // 2 - 4
+        o = oracle_render(scene, nx, ny, ns, seed=2024, chunk=1, rect=(x0, y0, 8, 8))
+        crop = g[y0:y0 + 8, x0:x0 + 8]
+        rms = gamma_rms(crop, o)
+        exact.append(float(np.mean(crop.view(np.uint32) == o.view(np.uint32))))
+        assert (rms <= TOL_RMS).all(), (x0, y0, rms)
+    print(f"{scene} {nx}x{ny}x{ns}: crops bit-exact fractions {exact}")
 
 
 @pytest.mark.parametrize("claim", ["1", "3", "16"])
@@ -274,11 +365,9 @@ def test_ppm_from_gpu_mean_matches_oracle_quantiser():
                                             ("random_motion", 40, 20, 8), ("earth", 32, 32, 8),
                                             ("edge_empty", 16, 8, 2), ("edge_single", 24, 12, 4),
                                             ("edge_degenerate", 40, 20, 8)])
-def test_engines_and_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
-    """The megakernel and the workgroup-wavefront engine (RTNW_ENGINE=wave) run the same
-    per-sample arithmetic and sum each work item in sample order, and the closest hit is
-    fixed by (t, list order) whatever the BVH's width: all four combinations must agree
-    bit for bit."""
+def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
+    """The closest hit is fixed by (t, list order) whatever the BVH's width
+    (RTNW_BVH_WIDTH=2 or 4 at scene creation): the images must agree bit for bit."""
     cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene]
     cam = rtnw.Camera.preset(cam_name, nx, ny)
     p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, chunk=4, seed=11)
@@ -286,9 +375,5 @@ def test_engines_and_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     for width in ("2", "4"):
         monkeypatch.setenv("RTNW_BVH_WIDTH", width)
         sc = rtnw.Scene.builtin(scene, earth_png=O.EARTH_PNG)   # the width is fixed when the scene is built
-        for engine in ("mega", "wave"):
-            monkeypatch.setenv("RTNW_ENGINE", engine)
-            out[(width, engine)] = sc.render_tile(cam, p, 0, 0, nx, ny)
-    ref = out[("2", "mega")]
-    for key, img in out.items():
-        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), key
+        out[width] = sc.render_tile(cam, p, 0, 0, nx, ny)
+    assert np.array_equal(out["4"].view(np.uint32), out["2"].view(np.uint32))

@@ -174,3 +174,60 @@ def test_bvh_builder_invariants(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.strip().endswith("OK")
+
+
+def test_c_pixel_interleave_matches_python_layout():
+    """rt_rank_pixels (the C ABI the RCCL driver uses) == rtnw.pixels_for_rank (bench.py,
+    tests): same factors, same pixels, same claim order; the ranks cover the image once."""
+    import ctypes
+    for world in (1, 2, 3, 4, 6, 8, 16):
+        a, b = ctypes.c_int(), ctypes.c_int()
+        rtnw.lib().rt_interleave_factors(world, ctypes.byref(a), ctypes.byref(b))
+        assert (a.value, b.value) == rtnw.interleave_factors(world)
+        for nx, ny in ((1000, 1000), (37, 23), (3, 2)):
+            seen = np.zeros((ny, nx), np.int32)
+            for r in range(world):
+                t = rtnw.rank_pixels_c(nx, ny, r, world)
+                assert np.array_equal(t, rtnw.pixels_for_rank(nx, ny, r, world)), (world, nx, ny, r)
+                seen[t[:, 1], t[:, 0]] += 1
+            assert (seen == 1).all()
+
+
+def test_c_unpack_matches_python_unpack():
+    import ctypes
+    nx, ny = 13, 7
+    rng = np.random.default_rng(1)
+    t = rtnw.pixels_for_rank(nx, ny, 1, 3)
+    packed = rng.random(len(t) * 3).astype(np.float32)
+    a = np.zeros((ny, nx, 3), np.float32)
+    b = np.zeros((ny, nx, 3), np.float32)
+    rtnw.unpack_tiles(packed, t, a)
+    assert rtnw.lib().rt_unpack_tiles(packed.ctypes.data, np.ascontiguousarray(t).ctypes.data, len(t), nx, ny,
+                                      b.ctypes.data) == 0
+    assert np.array_equal(a, b)
+    bad = np.array([[nx, 0, 1, 1]], np.int32)
+    assert rtnw.lib().rt_unpack_tiles(packed.ctypes.data, bad.ctypes.data, 1, nx, ny, b.ctypes.data) != 0
+
+
+def test_checkpoint_round_trip_and_corruption(tmp_path):
+    """rt_checkpoint_write / rt_checkpoint_read: header and sums survive, a flipped byte
+    or a truncated file is refused (checksum), and the write is an atomic replace."""
+    sums = np.arange(3 * 20 * 10, dtype=np.float32).reshape(10, 20, 3) * 0.25
+    p = rtnw.RenderParams(20, 10, 7, seed=99, max_depth=8, background=rtnw.RT_BG_SKY)
+    path = tmp_path / "a.rtck"
+    rtnw.write_checkpoint(str(path), sums, nx=20, ny=10, samples_done=7, params=p, job_hash=0xABCDEF)
+    assert not (tmp_path / "a.rtck.tmp").exists()
+    hdr, back = rtnw.read_checkpoint(str(path))
+    assert hdr["magic"] == rtnw.RT_CHECKPOINT_MAGIC and hdr["samples_done"] == 7 and hdr["seed"] == 99
+    assert hdr["max_depth"] == 8 and hdr["background"] == rtnw.RT_BG_SKY and hdr["job_hash"] == 0xABCDEF
+    assert np.array_equal(back, sums.ravel())
+    raw = bytearray(path.read_bytes())
+    raw[100] ^= 0x40
+    (tmp_path / "b.rtck").write_bytes(bytes(raw))
+    with pytest.raises(rtnw.RtError, match="checksum"):
+        rtnw.read_checkpoint(str(tmp_path / "b.rtck"))
+    (tmp_path / "c.rtck").write_bytes(path.read_bytes()[:-20])
+    with pytest.raises(rtnw.RtError):
+        rtnw.read_checkpoint(str(tmp_path / "c.rtck"))
+    with pytest.raises(rtnw.RtError):
+        rtnw.read_checkpoint(str(tmp_path / "missing.rtck"))

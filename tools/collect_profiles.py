@@ -46,7 +46,7 @@ def lanes(path):
     with open(path) as f:
         for r in csv.DictReader(f):
             n = r["Kernel_Name"]
-            if "rt_megakernel<false, false" not in n and "rt_wavefront<false, false" not in n:
+            if "rt_megakernel<false, false" not in n:
                 continue
             if d and r["Dispatch_Id"] != d["id"]:
                 continue   # the first timed dispatch only
@@ -57,7 +57,7 @@ def lanes(path):
 
 
 lines = ["# VALU lane utilisation (SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU), bench.py --spp 128"]
-for name, sub in (("megakernel", "pmc_l1"), ("wavefront engine (RTNW_ENGINE=wave)", "pmc_l2w")):
+for name, sub in (("megakernel", "pmc_l1"),):
     d = lanes(os.path.join(out, sub, "run_counter_collection.csv"))
     if not d:
         continue

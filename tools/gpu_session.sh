@@ -21,12 +21,12 @@ for step in "$@"; do
   case $step in
     build)  run build 600 python -c "import __graft_entry__ as g; g.build()" ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests)  run tests 1200 python -m pytest tests -m gpu -x -q -s ;;
+    tests)  run tests 1200 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread ;;
     testsk) run tests 1200 python -m pytest tests -m gpu -q -s ;;
     bench_small) run bench_small 600 python bench.py --spp 64 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench)  run bench 900 python bench.py ;;
     prof)   export TMPDIR=/tmp
-            run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+            run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --config ${BENCH_CFG:-c4} --steps 5 --warmup 1 --no-cpu-baseline ;;
     counters) export TMPDIR=/tmp; run counters 120 rocprofv3 -L ;;
     pmc_fetch) export TMPDIR=/tmp
             run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
@@ -40,11 +40,12 @@ for step in "$@"; do
     stages_cornell) run stages_cornell 600 python3 tools/stage_profile.py cornell_box ;;
     dist2)  run dist2 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --dist-backend gloo --spp 64 --steps 2 --warmup 1 --ppm gpurun_out/dist2.ppm ;;
     one_ppm) run one_ppm 600 python3 bench.py --spp 64 --steps 1 --warmup 0 --no-cpu-baseline --ppm gpurun_out/one.ppm ;;
-    pmc)    export TMPDIR=/tmp
-            run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
-            run pmc_write 900 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
-            run pmc_l2 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline
-            run pmc_sq 900 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmc)    export TMPDIR=/tmp   # BENCH_CFG=c4|c5|c2|c3 (default c4)
+            B="python3 bench.py --config ${BENCH_CFG:-c4} --steps 1 --warmup 0 --no-cpu-baseline"
+            run pmc_fetch 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- $B
+            run pmc_write 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- $B
+            run pmc_l2 300 timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmc_l2 -o run --output-format csv -- $B
+            run pmc_sq 300 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- $B ;;
     pmc_deep) export TMPDIR=/tmp
             B="python3 bench.py --spp ${PMC_SPP:-128} --steps 1 --warmup 0 --no-cpu-baseline"
             run pmc_d2 600 rocprofv3 --pmc TA_TA_BUSY GRBM_GUI_ACTIVE -d gpurun_out/pmc_d2 -o run --output-format csv -- $B
@@ -59,8 +60,7 @@ for step in "$@"; do
             python3 tools/pmc_deep.py gpurun_out > gpurun_out/pmc_deep.txt ;;
     pmc_lanes) export TMPDIR=/tmp
             B="python3 bench.py --spp ${PMC_SPP:-128} --steps 1 --warmup 0 --no-cpu-baseline"
-            run pmc_l1 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/pmc_l1 -o run --output-format csv -- $B
-            RTNW_ENGINE=wave run pmc_l2w 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/pmc_l2w -o run --output-format csv -- $B ;;
+            run pmc_l1 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/pmc_l1 -o run --output-format csv -- $B ;;
     ab)     run ab 1200 python3 tools/ab.py $AB_LIBS --rounds ${AB_ROUNDS:-2} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

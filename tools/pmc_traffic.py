@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""tools/pmc_traffic.py OUTDIR PROFILE_DIR — summarises rocprofv3 PMC passes of bench.py.
+"""tools/pmc_traffic.py OUTDIR PROFILE_DIR [SAMPLES] [CONFIG] — summarises rocprofv3 PMC passes of bench.py.
 
 Reads OUTDIR/pmc_{fetch,write,l2,sq}/run_counter_collection.csv (separate passes, as
 MI355X_MICROARCH.md §rocprofv3 requires: FETCH_SIZE and WRITE_SIZE do not fit one
@@ -7,12 +7,16 @@ pass), keeps the dispatches of the timed megakernel (rt_megakernel<false, false>
 and writes:
   PROFILE_DIR/traffic.json  hbm_bytes_per_launch / _per_sample for bench.py's roofline
   PROFILE_DIR/pmc_summary.md
+bench.py reads traffic.json for its roofline: VALU instructions per sample (the
+binding roof: wave-level SQ_INSTS_VALU, each 2 cycles on a SIMD-32), HBM bytes per
+sample, and lib_sha16 = the librt_hip.so build the counters were taken on.
 HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE/WRITE_SIZE are in KiB and
 gfx950's FETCH_SIZE reports half the bytes of wide reads (MI355X_MICROARCH.md §HBM);
 the doubling is uncalibrated for this kernel's scattered 16-B reads, so the read
 side is an upper estimate.
 """
 import csv
+import hashlib
 import json
 import os
 import sys
@@ -42,11 +46,17 @@ def first(rows):
 def main():
     out, prof = sys.argv[1], sys.argv[2]
     samples = float(sys.argv[3]) if len(sys.argv) > 3 else 500 * 500 * 1000
+    config = sys.argv[4] if len(sys.argv) > 4 else "c4"
     fetch = first(load(os.path.join(out, "pmc_fetch", "run_counter_collection.csv")))
     write = first(load(os.path.join(out, "pmc_write", "run_counter_collection.csv")))
     l2 = first(load(os.path.join(out, "pmc_l2", "run_counter_collection.csv")))
     sq = first(load(os.path.join(out, "pmc_sq", "run_counter_collection.csv")))
-    res = {"workload": "c4: final() 500x500 x 1000 spp (bench.py defaults)", "samples_per_launch": samples}
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "peter-shirley-ray-tracing-the-next-week_amd", "librt_hip.so")
+    with open(lib, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    res = {"config": config, "workload": f"{config} (bench.py --config {config})", "samples_per_launch": samples,
+           "lib_sha16": sha}
     if fetch and write:
         fb = fetch["FETCH_SIZE"] * 1024.0
         wb = write["WRITE_SIZE"] * 1024.0
@@ -58,7 +68,13 @@ def main():
         res["valu_active_per_wave_cycle"] = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
         res["wait_any_per_wave_cycle"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
         res["wait_inst_any_per_wave_cycle"] = sq["SQ_WAIT_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
-        res["valu_insts_per_sample_wave"] = sq["SQ_INSTS_VALU"] * 64 / samples
+        res["valu_insts_per_launch"] = sq["SQ_INSTS_VALU"]
+        res["valu_insts_per_sample"] = sq["SQ_INSTS_VALU"] / samples   # wave-level instructions
+        if "SQ_INSTS_SALU" in sq:
+            res["salu_insts_per_sample"] = sq["SQ_INSTS_SALU"] / samples
+        res["valu_issue_frac"] = sq["SQ_INSTS_VALU"] * 2 / (1024 * 2.4e9 * sq["dur_ns"] * 1e-9)
+        res["valu_issue_frac_at_measured_clock"] = sq["SQ_INSTS_VALU"] * 2 / (1024 * sq["GRBM_GUI_ACTIVE"] / 8)
+        res["kernel_ns_sq_pass"] = sq["dur_ns"]
         res["effective_clock_ghz"] = sq["GRBM_GUI_ACTIVE"] / 8 / sq["dur_ns"]
         res["waves"] = sq["SQ_WAVES"]
         res["rocprof_VGPR_Count"] = sq["vgpr"]   # rocprof's field (the code object says 128 VGPRs)

@@ -1,9 +1,7 @@
 #!/usr/bin/env python3
 """tools/stage_profile.py — where the engine's wave-cycles go (RT_FLAG_PROFILE
-build: s_memtime stamps at the stage boundaries, summed over waves).  Megakernel:
-claim / traverse / media / shade; wavefront engine (RTNW_ENGINE=wave): phase C /
-phase T / phase S / list building + barrier waits.  Diagnostic only: shares,
-never timings."""
+build: s_memtime stamps at the stage boundaries, summed over waves): claim /
+traverse / media / shade.  Diagnostic only: shares, never timings."""
 import json
 import os
 import sys
