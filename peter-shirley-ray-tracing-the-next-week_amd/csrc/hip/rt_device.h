@@ -489,10 +489,40 @@ __device__ __forceinline__ void cas(float &ka, uint32_t &ca, float &kb, uint32_t
 // One interior node: test the children, push the hit ones but the nearest far to
 // near (branch-free: a slot is written, then kept only if the child was hit; the
 // builder bounds sp by RT_STACK_DEPTH - 1), return the nearest (or empty).
-template <int kWidth>
-__device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, float best_t, uint32_t *stk, int &sp) {
+// Where a node step reads its node.  BVH2 nodes are 4 float4 (rt_layout.h); the
+// global reader fetches them from HBM (L1/L2), the LDS reader from the workgroup's
+// copy, stored as 4 planes of RT_LDS_NODE_CAP float4 (plane k holds float4 k of every
+// node) so one address register serves the 4 ds_read_b128 (immediate offsets) and
+// lanes reading different nodes spread over 16 bank windows instead of 4.
+typedef float F4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const F4v LdsF4;
+__device__ __forceinline__ float4 f4(F4v v) { return make_float4(v.x, v.y, v.z, v.w); }
+struct GlobalNodes {
+    const float4 *p;
+    __device__ __forceinline__ void load2(uint32_t n, float4 &b0, float4 &b1, float4 &b2, float4 &cf) const {
+        const float4 *N = p + n * 4;
+        b0 = N[0]; b1 = N[1]; b2 = N[2]; cf = N[3];
+    }
+    __device__ __forceinline__ const float4 *ptr4(uint32_t n) const { return p + n * 8; }
+};
+struct LdsNodes {
+    const LdsF4 *p;
+    __device__ __forceinline__ void load2(uint32_t n, float4 &b0, float4 &b1, float4 &b2, float4 &cf) const {
+        const LdsF4 *N = p + n;
+        b0 = f4(N[0]); b1 = f4(N[RT_LDS_NODE_CAP]); b2 = f4(N[2 * RT_LDS_NODE_CAP]); cf = f4(N[3 * RT_LDS_NODE_CAP]);
+    }
+    __device__ __forceinline__ const float4 *ptr4(uint32_t) const { return nullptr; }   // BVH4 stays in HBM
+};
+
+// One interior node: test the children, push the hit ones but the nearest far to
+// near (branch-free: a slot is written, then kept only if the child was hit; the
+// builder bounds sp by the BVH depth), return the nearest (or empty).
+template <int kWidth, class Nodes>
+__device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, const Slab &s, float best_t, uint32_t *stk,
+                                              int &sp) {
     if (kWidth == 2) {   // rt_dnode2
-        const float4 b0 = N[0], b1 = N[1], b2 = N[2], cf = N[3];
+        float4 b0, b1, b2, cf;
+        src.load2(node, b0, b1, b2, cf);
         const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
         const float k0 = box_entry<false>(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, c0);
         const float k1 = box_entry<false>(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, c1);
@@ -503,6 +533,7 @@ __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, fl
         sp += kf != RT_INF;
         return kn != RT_INF ? nearc : RT_EMPTY_CHILD;
     } else {             // rt_dnode4
+        const float4 *N = src.ptr4(node);
         const float4 qx01 = N[0], qx23 = N[1], qy01 = N[2], qy23 = N[3], qz01 = N[4], qz23 = N[5], cf = N[6];
         uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y), c2 = (uint32_t)fbits(cf.z),
                  c3 = (uint32_t)fbits(cf.w);
@@ -549,10 +580,9 @@ __device__ __forceinline__ uint32_t node_step(const float4 *N, const Slab &s, fl
 #ifndef RT_DESCEND_TAIL2
 #define RT_DESCEND_TAIL2 8
 #endif
-template <int kWidth, bool kCount, int kSteps = 1>
-__device__ __forceinline__ uint32_t descend(const float4 *nodes, uint32_t &node, const Slab &sl, float best_t,
+template <int kWidth, bool kCount, int kSteps = 1, class Nodes>
+__device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, const Slab &sl, float best_t,
                                             uint32_t *stk, int &sp, Counters &cnt) {
-    constexpr uint32_t kNodeStride = kWidth == 4 ? 8 : 4;   // float4 per node in HBM
     constexpr int kTail = kSteps == 1 ? RT_DESCEND_TAIL : RT_DESCEND_TAIL2;
     uint32_t pleaf = RT_EMPTY_CHILD;
     for (;;) {
@@ -560,7 +590,7 @@ __device__ __forceinline__ uint32_t descend(const float4 *nodes, uint32_t &node,
         for (int u = 0; u < kSteps; ++u) {
             if (!(node & RT_LEAF_BIT)) {
                 if (kCount) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
-                node = node_step<kWidth>(nodes + node * kNodeStride, sl, best_t, stk, sp);
+                node = node_step<kWidth>(nodes, node, sl, best_t, stk, sp);
             }
             const bool park = node != RT_EMPTY_CHILD && (node & RT_LEAF_BIT) && pleaf == RT_EMPTY_CHILD;
             pleaf = park ? node : pleaf;
@@ -826,9 +856,10 @@ struct MediumRec {
 #ifndef RT_LDS_MEDIA
 #define RT_LDS_MEDIA 8
 #endif
+template <int kBlock>
 __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds) {
     const int n = min(A.nmedia, RT_LDS_MEDIA);
-    for (int i = threadIdx.x; i < n; i += RT_BLOCK) {
+    for (int i = threadIdx.x; i < n; i += kBlock) {
         MediumRec m;
         m.md = A.media[i];
         m.g0 = A.bprims[m.md.x * 4 + 0];

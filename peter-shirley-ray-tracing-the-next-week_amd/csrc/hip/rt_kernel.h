@@ -4,7 +4,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define RT_BLOCK 256      // 4 waves per workgroup
+#define RT_BLOCK 256      // 4 waves per workgroup (BVH in HBM: 4 workgroups per CU)
+
+// LDS-resident BVH2 (RtKernelArgs.lds_nodes): one workgroup of 16 waves per CU holds
+// the scene's nodes in LDS as 4 planes of RT_LDS_NODE_CAP float4, beside the waves'
+// traversal stacks (RtKernelArgs.stack_depth entries per lane).
+#define RT_LDS_BLOCK 1024
+#define RT_LDS_NODE_CAP 1024
+#define RT_LDS_NODE_BYTES (4 * RT_LDS_NODE_CAP * 16)
+#define RT_LDS_STACK_BYTES(depth) ((RT_LDS_BLOCK / 64) * (depth) * 64 * 4)
+#define RT_LDS_BUDGET 163840   // LDS bytes per CU (160 KiB)
 
 // scene features a megakernel variant carries code for (rt_launch_megakernel)
 #define RT_FEAT_INST 1      // translate / rotate_y / flip_normals chains
@@ -31,6 +40,8 @@ struct RtKernelArgs {
     int nmedia;
     int features;           // RT_FEAT_* present in the scene (selects the megakernel variant)
     int need_dlen;          // |r.d| is used: media, metal / dielectric materials or the sky
+    int lds_nodes;          // 1: BVH2 nodes copied to LDS (RT_LDS_BLOCK workgroups, one per CU)
+    int stack_depth;        // traversal stack entries per lane of the LDS variant (BVH depth + 1)
     // camera (camera.h members)
     float org[3], llc[3], hor[3], ver[3], cu[3], cv[3];
     float lens, ct0, ct1;
@@ -62,3 +73,5 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
                                         const uint32_t *out_index, float *out, hipStream_t stream);
 // mode: 0 plain, 1 count, 2 profile; width: BVH width of the scene (2 or 4)
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);
+// Static LDS bytes of the LDS-BVH variant (its dynamic part: nodes + stacks).
+extern "C" int rt_megakernel_lds_static_bytes(void);

@@ -55,21 +55,40 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 // chains (cornell scenes), (u, v)-reading materials (earth()), checker textures
 // (the random scenes).  The host launches the smallest compiled variant covering
 // the scene (final(): none of them); RT_FEAT_ALL runs anything.
-template <bool kCount, bool kProf, int kWidth, int kFeat>
-__global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
+// kLds: the BVH2 nodes live in LDS (one workgroup of RT_LDS_BLOCK threads per CU
+// copies them at launch; node steps read them with ds_read_b128 instead of going
+// through L1/L2), the traversal stacks beside them with the scene's own depth.
+template <bool kCount, bool kProf, int kWidth, int kFeat, bool kLds>
+__global__ __launch_bounds__(kLds ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     constexpr bool kInst = (kFeat & RT_FEAT_INST) != 0, kUV = (kFeat & RT_FEAT_UV) != 0,
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0;
-    __shared__ uint32_t lds_stack[RT_BLOCK / 64][RT_STACK_DEPTH][64];
-    __shared__ CoopSlot lds_slots[RT_BLOCK / 64][64];
+    constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
+    __shared__ uint32_t lds_stack[kLds ? 1 : RT_BLOCK / 64][kLds ? 1 : RT_STACK_DEPTH][64];
+    __shared__ CoopSlot lds_slots[kBlock / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ CamV4 lds_cam[6];
+    extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
-    uint32_t *stk = &lds_stack[threadIdx.x >> 6][0][lane];
+    uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(lds_dyn + 4 * RT_LDS_NODE_CAP) +
+                               (threadIdx.x >> 6) * (uint32_t)A.stack_depth * 64u + lane
+                         : &lds_stack[threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
     // the media records are read from LDS (one broadcast read per medium)
-    load_media(A, lds_media);
+    load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) store_camera(A, lds_cam);
+    if (kLds) {
+        for (uint32_t i = threadIdx.x; i < A.nnodes; i += kBlock) {
+            const float4 *N = A.nodes + i * 4;
+            const float4 b0 = N[0], b1 = N[1], b2 = N[2], cf = N[3];
+            lds_dyn[i] = b0;
+            lds_dyn[i + RT_LDS_NODE_CAP] = b1;
+            lds_dyn[i + 2 * RT_LDS_NODE_CAP] = b2;
+            lds_dyn[i + 3 * RT_LDS_NODE_CAP] = cf;
+        }
+    }
     __syncthreads();
+    const GlobalNodes gnodes{A.nodes};
+    const LdsNodes lnodes{(const LdsF4 *)lds_dyn};
 
     const uint64_t skey = seed_key(A.seed);   // per-launch part of the sample keys
     // wave-uniform claim pool
@@ -220,7 +239,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtK
             if (phase == PH_TRAV) {
                 // the slab test needs no exact division: boxes are padded (bvh.cpp)
                 const Slab sl = make_slab(r, A.tmin);
-                const uint32_t pleaf = descend<kWidth, kCount, kInst ? 1 : 2>(A.nodes, node, sl, best_t, stk, sp, cnt);
+                uint32_t pleaf;
+                if constexpr (kLds)
+                    pleaf = descend<kWidth, kCount, kInst ? 1 : 2>(lnodes, node, sl, best_t, stk, sp, cnt);
+                else
+                    pleaf = descend<kWidth, kCount, kInst ? 1 : 2>(gnodes, node, sl, best_t, stk, sp, cnt);
                 if (pleaf != RT_EMPTY_CHILD) {
                     const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
                     // primitives in pairs: both 32-B heads are fetched before either test
@@ -358,28 +381,47 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
 }  // namespace
 
 // --------------------------------------------------------------- launchers
-template <int kWidth, int kFeat>
-static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
-    if (mode == 1)
-        hipLaunchKernelGGL((rt_megakernel<true, false, kWidth, kFeat>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
-    else if (mode == 2)
-        hipLaunchKernelGGL((rt_megakernel<false, true, kWidth, kFeat>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
-    else
-        hipLaunchKernelGGL((rt_megakernel<false, false, kWidth, kFeat>), dim3(grid), dim3(RT_BLOCK), 0, stream, *a);
+template <bool kCount, bool kProf, int kWidth, int kFeat, bool kLds>
+static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream) {
+    auto *k = rt_megakernel<kCount, kProf, kWidth, kFeat, kLds>;
+    size_t dyn = 0;
+    if (kLds) {
+        dyn = RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES(a->stack_depth);
+        static bool attr = false;   // dynamic LDS above the default limit, once per variant
+        if (!attr) {
+            hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               RT_LDS_BUDGET - rt_megakernel_lds_static_bytes());
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kLds ? RT_LDS_BLOCK : RT_BLOCK), dyn, stream, *a);
     return hipGetLastError();
 }
 
-// Compiled variants: every feature (any scene), none (final()), instances only
-// (cornell_box, cornell_smoke), checker only (the random scenes); BVH4 always runs
-// the all-feature variant.
-extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
-    if (a->bvh_width == 4) return launch_variant<4, RT_FEAT_ALL>(a, grid, mode, stream);
+template <int kWidth, int kFeat, bool kLds>
+static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
+    if (mode == 1) return launch_one<true, false, kWidth, kFeat, kLds>(a, grid, stream);
+    if (mode == 2) return launch_one<false, true, kWidth, kFeat, kLds>(a, grid, stream);
+    return launch_one<false, false, kWidth, kFeat, kLds>(a, grid, stream);
+}
+
+template <bool kLds>
+static hipError_t launch_features(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     switch (a->features) {
-    case 0: return launch_variant<2, 0>(a, grid, mode, stream);
-    case RT_FEAT_INST: return launch_variant<2, RT_FEAT_INST>(a, grid, mode, stream);
-    case RT_FEAT_CHECKER: return launch_variant<2, RT_FEAT_CHECKER>(a, grid, mode, stream);
-    default: return launch_variant<2, RT_FEAT_ALL>(a, grid, mode, stream);
+    case 0: return launch_variant<2, 0, kLds>(a, grid, mode, stream);
+    case RT_FEAT_INST: return launch_variant<2, RT_FEAT_INST, kLds>(a, grid, mode, stream);
+    case RT_FEAT_CHECKER: return launch_variant<2, RT_FEAT_CHECKER, kLds>(a, grid, mode, stream);
+    default: return launch_variant<2, RT_FEAT_ALL, kLds>(a, grid, mode, stream);
     }
+}
+
+// Compiled variants: every feature (any scene), none (final()), instances only
+// (cornell_box, cornell_smoke), checker only (the random scenes), each with the BVH2
+// in HBM or in LDS; BVH4 always runs the all-feature variant from HBM.
+extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
+    if (a->bvh_width == 4) return launch_variant<4, RT_FEAT_ALL, false>(a, grid, mode, stream);
+    return a->lds_nodes ? launch_features<true>(a, grid, mode, stream) : launch_features<false>(a, grid, mode, stream);
 }
 
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
@@ -392,12 +434,17 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
 template <int kWidth>
 static hipError_t occupancy_width(int *blocks_per_cu, int mode) {
     if (mode == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, RT_FEAT_ALL>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, RT_FEAT_ALL, false>, RT_BLOCK, 0);
     if (mode == 2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, RT_FEAT_ALL>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, RT_FEAT_ALL>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, RT_FEAT_ALL, false>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, RT_FEAT_ALL, false>, RT_BLOCK, 0);
 }
 
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width) {
     return width == 4 ? occupancy_width<4>(blocks_per_cu, mode) : occupancy_width<2>(blocks_per_cu, mode);
+}
+
+// the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
+extern "C" int rt_megakernel_lds_static_bytes(void) {
+    return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16) + 256;
 }

@@ -137,6 +137,8 @@ struct rt_scene {
     int device = 0;
     int cus = 0;
     int grid[3] = {0, 0, 0};      // persistent megakernel grid per variant (plain, count, profile)
+    bool lds_nodes = false;       // the BVH2 fits the LDS variant (one RT_LDS_BLOCK workgroup per CU)
+    int stack_depth = 0;          // its traversal stack entries per lane
     hipStream_t own_stream = nullptr;
     // scene in HBM: one allocation (arena) holding the arrays below
     void *arena = nullptr;
@@ -430,6 +432,20 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) bpc = std::min(bpc, std::max(1, std::atoi(e)));
         s->grid[mode] = std::max(1, bpc) * s->cus;
     }
+    // LDS-resident BVH2 (rt_kernel.h): nodes as 4 planes + one stack per lane of the
+    // scene's own depth, if both fit the CU's LDS beside the variant's static arrays.
+    // RTNW_LDS_BVH=0 keeps the nodes in HBM (A/B, tests).
+    {
+        s->stack_depth = s->bvh_depth + 1;
+        const long need = (long)RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES((long)s->stack_depth) +
+                          rt_megakernel_lds_static_bytes();
+        bool want = true;
+        if (const char *e = std::getenv("RTNW_LDS_BVH")) want = std::atoi(e) != 0;
+        s->lds_nodes = want && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
+                       s->nnodes <= RT_LDS_NODE_CAP && need <= RT_LDS_BUDGET;
+        if (s->lds_nodes)
+            for (int mode = 0; mode < 3; mode++) s->grid[mode] = s->cus;
+    }
     trace("device attributes");
     // the work counter (64 B) and the statistics counters in one allocation
     if ((e = hipMalloc(&s->counter, 64 + (RT_CNT_N + 16) * sizeof(unsigned long long))) != hipSuccess)
@@ -560,6 +576,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.has_bvh = s->has_bvh;
     a.nmedia = s->nmedia;
     a.need_dlen = s->nmedia > 0 || s->has_specular || p->background == RT_BG_SKY;
+    a.lds_nodes = s->lds_nodes ? 1 : 0;
+    a.stack_depth = s->stack_depth;
     a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
                  (s->has_checker ? RT_FEAT_CHECKER : 0);
     for (int k = 0; k < 3; k++) {
@@ -590,7 +608,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     // vec3::operator/= (vec3.h:134-141): col *= float(1.0 / ns)
     const uint32_t ns_total = sum_in ? p->sample_offset + (uint32_t)p->spp : (uint32_t)p->spp;
     const float k = (float)(1.0 / (double)(float)ns_total);
-    const uint64_t waves = (uint64_t)s->grid[mode] * (RT_BLOCK / 64);
+    const uint64_t waves = (uint64_t)s->grid[mode] * ((s->lds_nodes ? RT_LDS_BLOCK : RT_BLOCK) / 64);
     double kernel_ms = 0, resolve_ms = 0;
     for (uint64_t b = 0; b < nbatches; ++b) {
         const uint64_t c0 = b * per, c1 = std::min(c0 + per, nchunks_total);
