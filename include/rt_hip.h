@@ -202,6 +202,8 @@ typedef struct rt_stats {
     double lane_sphere_draw_trips;/*   lane-level rejection rounds */
     double chunk;                 /* samples per work item the launch used (rt_render_params.chunk or its default) */
     double batches;               /* megakernel launches (sample batches) the job took */
+    double lds_level;             /* scene data in LDS: 0 none (HBM, L1/L2), 1 the BVH2 nodes */
+    double stack_depth;           /* traversal stack entries per lane (LDS variants: the BVH depth + 1) */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */

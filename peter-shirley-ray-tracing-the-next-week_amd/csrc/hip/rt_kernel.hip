@@ -42,6 +42,11 @@ namespace {
 #define RT_READY_BATCH 48
 #endif
 
+// Node steps per descent exit check outside the instance variant (rt_device.h descend).
+#ifndef RT_DESCEND_STEPS
+#define RT_DESCEND_STEPS 2
+#endif
+
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -241,9 +246,9 @@ __global__ __launch_bounds__(kLds ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) 
                 const Slab sl = make_slab(r, A.tmin);
                 uint32_t pleaf;
                 if constexpr (kLds)
-                    pleaf = descend<kWidth, kCount, kInst ? 1 : 2>(lnodes, node, sl, best_t, stk, sp, cnt);
+                    pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt);
                 else
-                    pleaf = descend<kWidth, kCount, kInst ? 1 : 2>(gnodes, node, sl, best_t, stk, sp, cnt);
+                    pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt);
                 if (pleaf != RT_EMPTY_CHILD) {
                     const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
                     // primitives in pairs: both 32-B heads are fetched before either test

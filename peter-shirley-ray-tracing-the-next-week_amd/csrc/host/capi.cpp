@@ -434,7 +434,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     }
     // LDS-resident BVH2 (rt_kernel.h): nodes as 4 planes + one stack per lane of the
     // scene's own depth, if both fit the CU's LDS beside the variant's static arrays.
-    // RTNW_LDS_BVH=0 keeps the nodes in HBM (A/B, tests).
+    // RTNW_LDS_BVH=0 keeps the nodes in HBM (A/B, tests).  Primitive heads in LDS as
+    // well (with 16-bit stack entries to make room) measured no faster: 60.27 vs
+    // 60.29 ms on c4, both behind 32-bit entries with the nodes alone.
     {
         s->stack_depth = s->bvh_depth + 1;
         const long need = (long)RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES((long)s->stack_depth) +
@@ -683,6 +685,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->cycles_shade = (double)c[RT_CNT_N + 3];
         }
         stats->grid = (double)s->grid[mode];
+        stats->lds_level = s->lds_nodes ? 1.0 : 0.0;
+        stats->stack_depth = (double)(s->lds_nodes ? s->stack_depth : RT_STACK_DEPTH);
     }
     return RT_OK;
 }

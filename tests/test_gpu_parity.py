@@ -367,13 +367,21 @@ def test_ppm_from_gpu_mean_matches_oracle_quantiser():
                                             ("edge_degenerate", 40, 20, 8)])
 def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     """The closest hit is fixed by (t, list order) whatever the BVH's width
-    (RTNW_BVH_WIDTH=2 or 4 at scene creation): the images must agree bit for bit."""
+    (RTNW_BVH_WIDTH=2 or 4 at scene creation) and wherever its nodes are read from
+    (RTNW_LDS_BVH=1: the BVH2 copied to LDS, one 16-wave workgroup per CU; 0: HBM,
+    4-wave workgroups): the images must agree bit for bit."""
     cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene]
     cam = rtnw.Camera.preset(cam_name, nx, ny)
     p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, chunk=4, seed=11)
-    out = {}
-    for width in ("2", "4"):
+    out, levels = {}, {}
+    for width, lds in (("2", "1"), ("2", "0"), ("4", "1")):
         monkeypatch.setenv("RTNW_BVH_WIDTH", width)
-        sc = rtnw.Scene.builtin(scene, earth_png=O.EARTH_PNG)   # the width is fixed when the scene is built
-        out[width] = sc.render_tile(cam, p, 0, 0, nx, ny)
-    assert np.array_equal(out["4"].view(np.uint32), out["2"].view(np.uint32))
+        monkeypatch.setenv("RTNW_LDS_BVH", lds)
+        sc = rtnw.Scene.builtin(scene, earth_png=O.EARTH_PNG)   # fixed when the scene is built
+        img, st = sc.render_tile(cam, p, 0, 0, nx, ny, stats=True)
+        out[width, lds], levels[width, lds] = img, st["lds_level"]
+    # every scene with interior BVH nodes takes the LDS variant when allowed; BVH4 never
+    has_nodes = scene not in ("edge_empty", "edge_single", "earth")   # earth: one sphere, the root is a leaf
+    assert levels == {("2", "1"): float(has_nodes), ("2", "0"): 0.0, ("4", "1"): 0.0}
+    assert np.array_equal(out["2", "0"].view(np.uint32), out["2", "1"].view(np.uint32))
+    assert np.array_equal(out["4", "1"].view(np.uint32), out["2", "1"].view(np.uint32))

@@ -14,5 +14,5 @@ while [ $# -ge 2 ]; do
       -Rpass-analysis=kernel-resource-usage 2> ../variants/$name/resource.txt
   grep -A8 "ILb0ELb0" ../variants/$name/resource.txt | grep -E "VGPRs:|Scratch" | sed "s/.*remark: */$name: /"
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../variants/$name/librt_hip.so ../variants/$name/rt_kernel.o \
-      build/capi.o build/bvh.o build/flatten.o build/rtnw.o build/png.o -lz -Wl,-rpath,/opt/rocm/lib
+      build/capi.o build/bvh.o build/flatten.o build/rtnw.o build/png.o build/dist.o -lz -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 done
