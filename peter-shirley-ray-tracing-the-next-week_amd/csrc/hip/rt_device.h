@@ -524,14 +524,20 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
         float4 b0, b1, b2, cf;
         src.load2(node, b0, b1, b2, cf);
         const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-        const float k0 = box_entry<false>(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, c0);
-        const float k1 = box_entry<false>(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, c1);
-        const bool second = k1 < k0;   // ties: child 0 first
-        const uint32_t nearc = second ? c1 : c0, farc = second ? c0 : c1;
-        const float kn = second ? k1 : k0, kf = second ? k0 : k1;
-        stk[sp * 64] = farc;
-        sp += kf != RT_INF;
-        return kn != RT_INF ? nearc : RT_EMPTY_CHILD;
+        // hit flags and the order as lane masks (SALU), not +inf entry keys compared
+        // and selected per lane: 3 compares instead of 5 compares and 7 selects, and
+        // no compare -> select hazard waits (s_nop) between them
+        float tn0, tf0, tn1, tf1;
+        box_span(s, F2{b0.x, b0.y}, F2{b0.z, b0.w}, F2{b1.x, b1.y}, best_t, tn0, tf0);
+        box_span(s, F2{b1.z, b1.w}, F2{b2.x, b2.y}, F2{b2.z, b2.w}, best_t, tn1, tf1);
+        const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;   // a hit's entry is finite (tf <= best_t)
+        const bool lt = tn1 < tn0;
+        const bool second = h1 & (!h0 | lt);           // ties: child 0 first (no short circuit: no branch)
+        const uint32_t nearc = second ? c1 : (h0 ? c0 : RT_EMPTY_CHILD), farc = second ? c0 : c1;
+        stk[sp * 64] = farc;                           // kept only if both children were hit
+        const int sp0 = h0 ? sp + 1 : sp;
+        sp = h1 ? sp0 : sp;
+        return nearc;
     } else {             // rt_dnode4
         const float4 *N = src.ptr4(node);
         const float4 qx01 = N[0], qx23 = N[1], qy01 = N[2], qy23 = N[3], qz01 = N[4], qz23 = N[5], cf = N[6];
