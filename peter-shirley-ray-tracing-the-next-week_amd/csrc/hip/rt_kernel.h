@@ -40,6 +40,10 @@ struct RtKernelArgs {
     int nmedia;
     int features;           // RT_FEAT_* present in the scene (selects the megakernel variant)
     int need_dlen;          // |r.d| is used: media, metal / dielectric materials or the sky
+    const float4 *groups;   // flat scan: 3 x float4 per group (rt_dgroup)
+    int ngroups;
+    int scan;               // 1: flat scan of the groups instead of a BVH (small scenes, rt_layout.h)
+    uint32_t nprims;        // surface primitives (flat scan: all copied to LDS)
     int lds_nodes;          // 1: BVH2 nodes copied to LDS (RT_LDS_BLOCK workgroups, one per CU)
     int stack_depth;        // traversal stack entries per lane of the LDS variant (BVH depth + 1)
     // camera (camera.h members)
@@ -71,7 +75,7 @@ extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int 
 #define RT_RESOLVE_RAW 8      // write the sums themselves (checkpoints), not sum * k
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
-// mode: 0 plain, 1 count, 2 profile; width: BVH width of the scene (2 or 4)
+// mode: 0 plain, 1 count, 2 profile; width: BVH width of the scene (2 or 4), 0: the flat-scan kernel
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);
 // Static LDS bytes of the LDS-BVH variant (its dynamic part: nodes + stacks).
 extern "C" int rt_megakernel_lds_static_bytes(void);

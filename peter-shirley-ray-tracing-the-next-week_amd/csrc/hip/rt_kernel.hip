@@ -60,15 +60,20 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 // chains (cornell scenes), (u, v)-reading materials (earth()), checker textures
 // (the random scenes).  The host launches the smallest compiled variant covering
 // the scene (final(): none of them); RT_FEAT_ALL runs anything.
-// kLds: the BVH2 nodes live in LDS (one workgroup of RT_LDS_BLOCK threads per CU
-// copies them at launch; node steps read them with ds_read_b128 instead of going
-// through L1/L2), the traversal stacks beside them with the scene's own depth.
-template <bool kCount, bool kProf, int kWidth, int kFeat, bool kLds>
-__global__ __launch_bounds__(kLds ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
+// kMode, the closest-hit search:
+//   0  BVH in HBM (nodes through L1/L2), 4-wave workgroups, 24-entry LDS stacks;
+//   1  BVH2 nodes in LDS (one workgroup of RT_LDS_BLOCK threads per CU copies them
+//      at launch; node steps read them with ds_read_b128), stacks of the scene's depth;
+//   2  flat scan of the primitive groups (rt_layout.h rt_dgroup), primitives in LDS,
+//      no BVH and no stack: scenes of at most RT_SCAN_MAX primitives.
+template <bool kCount, bool kProf, int kWidth, int kFeat, int kMode>
+__global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     constexpr bool kInst = (kFeat & RT_FEAT_INST) != 0, kUV = (kFeat & RT_FEAT_UV) != 0,
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0;
+    constexpr bool kLds = kMode == 1, kScan = kMode == 2;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
-    __shared__ uint32_t lds_stack[kLds ? 1 : RT_BLOCK / 64][kLds ? 1 : RT_STACK_DEPTH][64];
+    __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : RT_STACK_DEPTH][64];
+    __shared__ float4 lds_scan[kScan ? 7 * RT_SCAN_MAX : 1];   // kScan: 4 float4 per primitive, 3 per group
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ CamV4 lds_cam[6];
@@ -76,7 +81,7 @@ __global__ __launch_bounds__(kLds ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) 
     const uint32_t lane = lane_id();
     uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(lds_dyn + 4 * RT_LDS_NODE_CAP) +
                                (threadIdx.x >> 6) * (uint32_t)A.stack_depth * 64u + lane
-                         : &lds_stack[threadIdx.x >> 6][0][lane];
+                         : &lds_stack[kMode ? 0 : threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
     // the media records are read from LDS (one broadcast read per medium)
     load_media<kBlock>(A, lds_media);
@@ -90,6 +95,10 @@ __global__ __launch_bounds__(kLds ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) 
             lds_dyn[i + 2 * RT_LDS_NODE_CAP] = b2;
             lds_dyn[i + 3 * RT_LDS_NODE_CAP] = cf;
         }
+    }
+    if (kScan) {
+        for (int i = threadIdx.x; i < 4 * (int)A.nprims; i += kBlock) lds_scan[i] = A.prims[i];
+        for (int i = threadIdx.x; i < 3 * A.ngroups; i += kBlock) lds_scan[4 * RT_SCAN_MAX + i] = A.groups[i];
     }
     __syncthreads();
     const GlobalNodes gnodes{A.nodes};
@@ -238,42 +247,90 @@ __global__ __launch_bounds__(kLds ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) 
         // RT_READY_BATCH lanes have their hit, then shades that batch: a lane that
         // finished early no longer holds the wave in traversal, and a lane still
         // searching keeps its LDS stack and carries on in the next iteration.
-        for (;;) {
-            if (__ballot(phase == PH_TRAV) == 0ull) break;
-            if (__popcll(__ballot(phase == PH_READY)) >= RT_READY_BATCH) break;
-            if (phase == PH_TRAV) {
-                // the slab test needs no exact division: boxes are padded (bvh.cpp)
+        if constexpr (kScan) {
+            // ---- 3'. closest surface hit, flat scan: every lane with a new segment,
+            // group by group (box test for all lanes, skipped when none hits; one
+            // object-space transform per group), primitive by primitive in lockstep.
+            const bool act = phase == PH_TRAV;
+            if (__ballot(act) != 0ull) {
+                typedef __attribute__((address_space(3))) const F4v LdsScan;
+                const LdsScan *P = (const LdsScan *)lds_scan;
+                const LdsScan *G = P + 4 * RT_SCAN_MAX;
                 const Slab sl = make_slab(r, A.tmin);
-                uint32_t pleaf;
-                if constexpr (kLds)
-                    pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt);
-                else
-                    pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt);
-                if (pleaf != RT_EMPTY_CHILD) {
-                    const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
-                    // primitives in pairs: both 32-B heads are fetched before either test
-                    for (uint32_t q = 0; q < nleaf; q += 2) {
-                        const uint32_t ia = first + q;
-                        const bool two = q + 1 < nleaf;
-                        const uint32_t ib = two ? ia + 1 : ia;
-                        const float4 ga = A.prims[ia * 4 + 0], ma = A.prims[ia * 4 + 1];
-                        const float4 gb = A.prims[ib * 4 + 0], mb = A.prims[ib * 4 + 1];
-                        int key, kind;
-                        float t = prim_t_head<kInst>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
-                        if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                        if (t < best_t || (t == best_t && key < best_key)) {
-                            best_t = t; best_key = key; best_prim = ia;
+                for (int gi = 0; gi < A.ngroups; ++gi) {
+                    const F4v gh = G[3 * gi], bx = G[3 * gi + 1], bz = G[3 * gi + 2];
+                    float tn, tf;
+                    box_span(sl, F2{bx.x, bx.y}, F2{bx.z, bx.w}, F2{bz.x, bz.y}, best_t, tn, tf);
+                    const bool in = act && tn <= tf;
+                    if (kCount && act) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
+                    if (__ballot(in) == 0ull) continue;
+                    const int first = __builtin_amdgcn_readfirstlane(fbits(gh.x));
+                    const int count = __builtin_amdgcn_readfirstlane(fbits(gh.y));
+                    const int inst = __builtin_amdgcn_readfirstlane(fbits(gh.z));
+                    Ray ro = r;
+                    if (kInst && inst >= 0) ro = to_object(A.insts, inst, r);
+                    for (int q = first; q < first + count; ++q) {
+                        const F4v g0v = P[4 * q], mmv = P[4 * q + 1];
+                        const float4 g0 = f4(g0v);
+                        const int m0 = __builtin_amdgcn_readfirstlane(fbits(mmv.x));
+                        const int kind = m0 & 0xff;
+                        float t;
+                        if (kind == RT_PRIM_SPHERE) {
+                            t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, ro, A.tmin);
+                        } else if (kind == RT_PRIM_MOVING_SPHERE) {
+                            t = sphere_t(msphere_center(g0, f4(P[4 * q + 2]), f4(P[4 * q + 3]), ro.time), g0.w, ro, A.tmin);
+                        } else {
+                            t = rect_t(kind, g0, mmv.y, ro, A.tmin);
                         }
-                        if (two) {
-                            t = prim_t_head<kInst>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
-                            if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                            if (t < best_t || (t == best_t && key < best_key)) {
-                                best_t = t; best_key = key; best_prim = ib;
-                            }
+                        const int order = fbits(mmv.w);
+                        const int key = kind <= RT_PRIM_MOVING_SPHERE ? order : -1 - order;
+                        if (kCount && in) cnt.prim(kind | (kInst && inst >= 0 ? 0x100 : 0));
+                        if (kCount && first_active()) cnt.w_prims++;
+                        if (in && (t < best_t || (t == best_t && key < best_key))) {
+                            best_t = t; best_key = key; best_prim = (uint32_t)q;
                         }
                     }
                 }
-                if (node == RT_EMPTY_CHILD) phase = PH_READY;   // stack empty too (popped above)
+                if (act) phase = PH_READY;
+            }
+        } else {
+            for (;;) {
+                if (__ballot(phase == PH_TRAV) == 0ull) break;
+                if (__popcll(__ballot(phase == PH_READY)) >= RT_READY_BATCH) break;
+                if (phase == PH_TRAV) {
+                    // the slab test needs no exact division: boxes are padded (bvh.cpp)
+                    const Slab sl = make_slab(r, A.tmin);
+                    uint32_t pleaf;
+                    if constexpr (kLds)
+                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt);
+                    else
+                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt);
+                    if (pleaf != RT_EMPTY_CHILD) {
+                        const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
+                        // primitives in pairs: both 32-B heads are fetched before either test
+                        for (uint32_t q = 0; q < nleaf; q += 2) {
+                            const uint32_t ia = first + q;
+                            const bool two = q + 1 < nleaf;
+                            const uint32_t ib = two ? ia + 1 : ia;
+                            const float4 ga = A.prims[ia * 4 + 0], ma = A.prims[ia * 4 + 1];
+                            const float4 gb = A.prims[ib * 4 + 0], mb = A.prims[ib * 4 + 1];
+                            int key, kind;
+                            float t = prim_t_head<kInst>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
+                            if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
+                            if (t < best_t || (t == best_t && key < best_key)) {
+                                best_t = t; best_key = key; best_prim = ia;
+                            }
+                            if (two) {
+                                t = prim_t_head<kInst>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
+                                if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
+                                if (t < best_t || (t == best_t && key < best_key)) {
+                                    best_t = t; best_key = key; best_prim = ib;
+                                }
+                            }
+                        }
+                    }
+                    if (node == RT_EMPTY_CHILD) phase = PH_READY;   // stack empty too (popped above)
+                }
             }
         }
         mark(1);
@@ -386,11 +443,11 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
 }  // namespace
 
 // --------------------------------------------------------------- launchers
-template <bool kCount, bool kProf, int kWidth, int kFeat, bool kLds>
+template <bool kCount, bool kProf, int kWidth, int kFeat, int kLds>
 static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream) {
     auto *k = rt_megakernel<kCount, kProf, kWidth, kFeat, kLds>;
     size_t dyn = 0;
-    if (kLds) {
+    if (kLds == 1) {
         dyn = RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES(a->stack_depth);
         static bool attr = false;   // dynamic LDS above the default limit, once per variant
         if (!attr) {
@@ -400,18 +457,18 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
             attr = true;
         }
     }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kLds ? RT_LDS_BLOCK : RT_BLOCK), dyn, stream, *a);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kLds == 1 ? RT_LDS_BLOCK : RT_BLOCK), dyn, stream, *a);
     return hipGetLastError();
 }
 
-template <int kWidth, int kFeat, bool kLds>
+template <int kWidth, int kFeat, int kLds>
 static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (mode == 1) return launch_one<true, false, kWidth, kFeat, kLds>(a, grid, stream);
     if (mode == 2) return launch_one<false, true, kWidth, kFeat, kLds>(a, grid, stream);
     return launch_one<false, false, kWidth, kFeat, kLds>(a, grid, stream);
 }
 
-template <bool kLds>
+template <int kLds>
 static hipError_t launch_features(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     switch (a->features) {
     case 0: return launch_variant<2, 0, kLds>(a, grid, mode, stream);
@@ -425,8 +482,9 @@ static hipError_t launch_features(const RtKernelArgs *a, int grid, int mode, hip
 // (cornell_box, cornell_smoke), checker only (the random scenes), each with the BVH2
 // in HBM or in LDS; BVH4 always runs the all-feature variant from HBM.
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
-    if (a->bvh_width == 4) return launch_variant<4, RT_FEAT_ALL, false>(a, grid, mode, stream);
-    return a->lds_nodes ? launch_features<true>(a, grid, mode, stream) : launch_features<false>(a, grid, mode, stream);
+    if (a->scan) return launch_features<2>(a, grid, mode, stream);
+    if (a->bvh_width == 4) return launch_variant<4, RT_FEAT_ALL, 0>(a, grid, mode, stream);
+    return a->lds_nodes ? launch_features<1>(a, grid, mode, stream) : launch_features<0>(a, grid, mode, stream);
 }
 
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
@@ -436,17 +494,18 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
     return hipGetLastError();
 }
 
-template <int kWidth>
+template <int kWidth, int kMode>
 static hipError_t occupancy_width(int *blocks_per_cu, int mode) {
     if (mode == 1)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, RT_FEAT_ALL, false>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<true, false, kWidth, RT_FEAT_ALL, kMode>, RT_BLOCK, 0);
     if (mode == 2)
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, RT_FEAT_ALL, false>, RT_BLOCK, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, RT_FEAT_ALL, false>, RT_BLOCK, 0);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, true, kWidth, RT_FEAT_ALL, kMode>, RT_BLOCK, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rt_megakernel<false, false, kWidth, RT_FEAT_ALL, kMode>, RT_BLOCK, 0);
 }
 
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width) {
-    return width == 4 ? occupancy_width<4>(blocks_per_cu, mode) : occupancy_width<2>(blocks_per_cu, mode);
+    if (width == 0) return occupancy_width<2, 2>(blocks_per_cu, mode);
+    return width == 4 ? occupancy_width<4, 0>(blocks_per_cu, mode) : occupancy_width<2, 0>(blocks_per_cu, mode);
 }
 
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera

@@ -338,6 +338,11 @@ struct Collapser {
 
 }  // namespace
 
+void prim_bounds(const rt_prim &p, const rt_instance *instances, float time0, float time1, float lo[3], float hi[3]) {
+    const Box b = prim_box(p, instances, std::min(0.0, (double)time0), std::max(0.0, (double)time1));
+    float_box(b, lo, hi);
+}
+
 BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, float time0, float time1) {
     BvhResult res;
     if (n <= 0) return res;

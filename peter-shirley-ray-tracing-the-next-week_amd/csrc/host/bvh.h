@@ -21,4 +21,8 @@ struct BvhResult {
 // width: 2 or 4 (RTNW_BVH_WIDTH overrides).
 BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, float time0, float time1);
 
+// World-space box of one primitive over the shutter span [min(0, time0), max(0, time1)],
+// padded like the BVH's boxes and rounded outward to float.
+void prim_bounds(const rt_prim &p, const rt_instance *instances, float time0, float time1, float lo[3], float hi[3]);
+
 }  // namespace rtnw

@@ -74,9 +74,9 @@ int commit(Arena &a, void **base) {
 // property of the code objects, queried once per process.
 hipError_t occupancy(int *mega, int mode, int width) {
     static std::mutex mu;
-    static int cache[3][2] = {};
+    static int cache[3][3] = {};   // [mode][BVH2, BVH4, flat scan]
     std::lock_guard<std::mutex> lock(mu);
-    int &c = cache[mode][width == 4 ? 1 : 0];
+    int &c = cache[mode][width == 4 ? 1 : (width == 0 ? 2 : 0)];
     if (!c) {
         hipError_t e;
         if ((e = rt_megakernel_occupancy(&c, mode, width)) != hipSuccess) { c = 0; return e; }
@@ -143,7 +143,9 @@ struct rt_scene {
     // scene in HBM: one allocation (arena) holding the arrays below
     void *arena = nullptr;
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
-         *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr;
+         *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr, *groups = nullptr;
+    bool scan = false;            // flat scan of the primitive groups instead of the BVH (small scenes)
+    int ngroups = 0;
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
     bool has_moving = false;
@@ -316,9 +318,43 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->time1 = d->time1;
     auto cleanup = [&](int rc) { rt_scene_destroy(s); return rc; };
 
+    // Flat scan instead of the BVH for scenes of at most RT_SCAN_MAX primitives
+    // (rt_layout.h rt_dgroup; RTNW_SCAN=0 keeps the BVH): primitives ordered by
+    // instance chain (list order within a chain), one group per chain.
+    {
+        bool want = true;
+        if (const char *e = std::getenv("RTNW_SCAN")) want = std::atoi(e) != 0;
+        s->scan = want && d->nprims >= 1 && d->nprims <= RT_SCAN_MAX && bvh.width == 2;
+    }
+    std::vector<int> order = bvh.order;
+    std::vector<rt_dgroup> groups;
+    if (s->scan) {
+        order.resize(d->nprims);
+        for (int i = 0; i < d->nprims; i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int x, int y) { return d->prims[x].instance < d->prims[y].instance; });
+        for (int i = 0; i < d->nprims; i++) {
+            const rt_prim &pr = d->prims[order[i]];
+            float lo[3], hi[3];
+            rtnw::prim_bounds(pr, d->instances, d->time0, d->time1, lo, hi);
+            if (groups.empty() || groups.back().instance != pr.instance) {
+                rt_dgroup g{};
+                g.first = i;
+                g.instance = pr.instance;
+                g.bx[0] = lo[0]; g.bx[1] = hi[0]; g.bx[2] = lo[1]; g.bx[3] = hi[1];
+                g.bz[0] = lo[2]; g.bz[1] = hi[2];
+                groups.push_back(g);
+            }
+            rt_dgroup &g = groups.back();
+            g.count++;
+            g.bx[0] = std::min(g.bx[0], lo[0]); g.bx[1] = std::max(g.bx[1], hi[0]);
+            g.bx[2] = std::min(g.bx[2], lo[1]); g.bx[3] = std::max(g.bx[3], hi[1]);
+            g.bz[0] = std::min(g.bz[0], lo[2]); g.bz[1] = std::max(g.bz[1], hi[2]);
+        }
+    }
     std::vector<rt_dprim> prims(d->nprims), bprims(d->nboundary);
     for (int i = 0; i < d->nprims; i++) {
-        const int src = bvh.order[i];
+        const int src = order[i];
         prims[i] = to_dprim(d->prims[src], src);
         s->has_moving |= d->prims[src].kind == RT_PRIM_MOVING_SPHERE;
     }
@@ -408,6 +444,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     stage(arena, &s->mats, mats);
     stage(arena, &s->texs, texs);
     stage(arena, &s->insts, insts);
+    stage(arena, &s->groups, groups);
     stage(arena, &s->ranvec, ranvec);
     stage(arena, &s->perm, perm);
     stage(arena, &s->texels, texels);
@@ -422,12 +459,14 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->bvh_width = bvh.width;
     s->nprims = d->nprims;
     s->ninstances = d->ninstances;
+    s->ngroups = (int)groups.size();
 
     if ((e = hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return cleanup(hip_fail(e, "hipDeviceGetAttribute"));
     for (int mode = 0; mode < 3; mode++) {
         int bpc = 0;
-        if ((e = occupancy(&bpc, mode, s->bvh_width)) != hipSuccess) return cleanup(hip_fail(e, "occupancy query"));
+        if ((e = occupancy(&bpc, mode, s->scan ? 0 : s->bvh_width)) != hipSuccess)
+            return cleanup(hip_fail(e, "occupancy query"));
         // RTNW_BLOCKS_PER_CU caps the resident workgroups per CU (occupancy experiments only)
         if (const char *e = std::getenv("RTNW_BLOCKS_PER_CU")) bpc = std::min(bpc, std::max(1, std::atoi(e)));
         s->grid[mode] = std::max(1, bpc) * s->cus;
@@ -443,7 +482,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
                           rt_megakernel_lds_static_bytes();
         bool want = true;
         if (const char *e = std::getenv("RTNW_LDS_BVH")) want = std::atoi(e) != 0;
-        s->lds_nodes = want && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
+        s->lds_nodes = want && !s->scan && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
                        s->nnodes <= RT_LDS_NODE_CAP && need <= RT_LDS_BUDGET;
         if (s->lds_nodes)
             for (int mode = 0; mode < 3; mode++) s->grid[mode] = s->cus;
@@ -579,6 +618,10 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.nmedia = s->nmedia;
     a.need_dlen = s->nmedia > 0 || s->has_specular || p->background == RT_BG_SKY;
     a.lds_nodes = s->lds_nodes ? 1 : 0;
+    a.scan = s->scan ? 1 : 0;
+    a.groups = (const float4 *)s->groups;
+    a.ngroups = s->ngroups;
+    a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
                  (s->has_checker ? RT_FEAT_CHECKER : 0);
@@ -686,6 +729,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         }
         stats->grid = (double)s->grid[mode];
         stats->lds_level = s->lds_nodes ? 1.0 : 0.0;
+        stats->scan_groups = s->scan ? (double)s->ngroups : 0.0;
         stats->stack_depth = (double)(s->lds_nodes ? s->stack_depth : RT_STACK_DEPTH);
     }
     return RT_OK;

@@ -67,6 +67,19 @@ struct rt_dprim {
     float g1[4], g2[4];
 };
 
+// Flat scan (scenes of at most RT_SCAN_MAX surface primitives, capi.cpp): the
+// primitives are ordered by instance chain, and each run of one chain is a group,
+// 48 B: (first, count, instance (-1 none), -) + its world box as in a BVH node,
+// (lo.x, hi.x, lo.y, hi.y), (lo.z, hi.z, -, -).  A wave tests every group's box
+// against all its rays at once, transforms its rays into the group's object space
+// ONCE, and tests the group's primitives in lockstep (every lane the same one):
+// the instance level of a two-level structure, without per-leaf transforms.
+#define RT_SCAN_MAX 64
+struct rt_dgroup {
+    int32_t first, count, instance, pad;
+    float bx[4], bz[4];
+};
+
 // Material, 32 B: (kind, texture, fuzz, ref_idx) + (albedo.xyz, flags).  A dielectric
 // carries (float)(1.0/(double)ref_idx), schlick r0^2 and ref_idx^2 in albedo (capi.cpp).
 struct rt_dmaterial {

@@ -366,22 +366,29 @@ def test_ppm_from_gpu_mean_matches_oracle_quantiser():
                                             ("edge_empty", 16, 8, 2), ("edge_single", 24, 12, 4),
                                             ("edge_degenerate", 40, 20, 8)])
 def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
-    """The closest hit is fixed by (t, list order) whatever the BVH's width
-    (RTNW_BVH_WIDTH=2 or 4 at scene creation) and wherever its nodes are read from
-    (RTNW_LDS_BVH=1: the BVH2 copied to LDS, one 16-wave workgroup per CU; 0: HBM,
-    4-wave workgroups): the images must agree bit for bit."""
+    """The closest hit is fixed by (t, list order) whatever structure finds it: the
+    BVH's width (RTNW_BVH_WIDTH=2 or 4 at scene creation), where its nodes are read
+    from (RTNW_LDS_BVH=1: the BVH2 copied to LDS, one 16-wave workgroup per CU; 0:
+    HBM, 4-wave workgroups), or no BVH at all (the flat scan of instance groups that
+    scenes of <= 64 primitives take unless RTNW_SCAN=0): the images must agree bit
+    for bit."""
     cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene]
     cam = rtnw.Camera.preset(cam_name, nx, ny)
     p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, chunk=4, seed=11)
-    out, levels = {}, {}
-    for width, lds in (("2", "1"), ("2", "0"), ("4", "1")):
+    out, how = {}, {}
+    for width, lds, scan in (("2", "1", "1"), ("2", "1", "0"), ("2", "0", "0"), ("4", "1", "1")):
         monkeypatch.setenv("RTNW_BVH_WIDTH", width)
         monkeypatch.setenv("RTNW_LDS_BVH", lds)
+        monkeypatch.setenv("RTNW_SCAN", scan)
         sc = rtnw.Scene.builtin(scene, earth_png=O.EARTH_PNG)   # fixed when the scene is built
         img, st = sc.render_tile(cam, p, 0, 0, nx, ny, stats=True)
-        out[width, lds], levels[width, lds] = img, st["lds_level"]
-    # every scene with interior BVH nodes takes the LDS variant when allowed; BVH4 never
+        out[width, lds, scan], how[width, lds, scan] = img, (st["lds_level"], st["scan_groups"] > 0)
+    small = scene != "final" and scene != "random_motion"       # <= 64 primitives: scanned by default
     has_nodes = scene not in ("edge_empty", "edge_single", "earth")   # earth: one sphere, the root is a leaf
-    assert levels == {("2", "1"): float(has_nodes), ("2", "0"): 0.0, ("4", "1"): 0.0}
-    assert np.array_equal(out["2", "0"].view(np.uint32), out["2", "1"].view(np.uint32))
-    assert np.array_equal(out["4", "1"].view(np.uint32), out["2", "1"].view(np.uint32))
+    nonempty = scene != "edge_empty"
+    assert how == {("2", "1", "1"): (0.0, nonempty) if small else (1.0, False),
+                   ("2", "1", "0"): (float(has_nodes), False), ("2", "0", "0"): (0.0, False),
+                   ("4", "1", "1"): (0.0, False)}, how
+    ref = out["2", "0", "0"].view(np.uint32)
+    for k, img in out.items():
+        assert np.array_equal(img.view(np.uint32), ref), k
