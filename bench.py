@@ -317,7 +317,7 @@ def main():
     sha = lib_sha16()
     roof = {"bound": "valu_issue", "achieved": None, "peak": VALU_PEAK / 1e9, "unit": "G wave-VALU-instr/s",
             "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
-            "lds_level": int(st["lds_level"]), "stack_depth": int(st["stack_depth"]), "scan_groups": int(st["scan_groups"]),
+            "lds_level": int(st["lds_level"]), "stack_depth": int(st["stack_depth"]), "scan_groups": int(st["scan_groups"]), "prescan": int(st["prescan"]),
             "batches_per_step": int(st["batches"]),
             "valu_insts_per_sample": None, "profile": None, "profile_matches_library": None,
             "cache_served_bytes_per_launch": cache_bytes,

@@ -205,6 +205,7 @@ typedef struct rt_stats {
     double lds_level;             /* scene data in LDS: 0 none (HBM, L1/L2), 1 the BVH2 nodes */
     double stack_depth;           /* traversal stack entries per lane (LDS variants: the BVH depth + 1) */
     double scan_groups;           /* flat scan instead of a BVH (<= 64 primitives): its instance groups, else 0 */
+    double prescan;               /* BVH scenes: largest primitives kept out of the BVH, tested first in lockstep */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */

@@ -845,6 +845,43 @@ __device__ __forceinline__ CamView load_camera(const CamV4 *lds) {
     return C;
 }
 
+// ------------------------------------------------------- lockstep primitives
+// Tests primitives [first, first + count) of an LDS copy (4 float4 each, the HBM
+// record) against every lane's ray in lockstep: the primitive, its kind and its
+// instance are the same in all lanes (broadcast reads, scalar branches), so only
+// the kind's own test runs and no lane idles behind another's traversal.  Lanes
+// with `in` false compute but keep nothing.  kPerPrimInst: each primitive's own
+// instance chain (pre-scan); otherwise the caller transformed `r` for the group.
+typedef __attribute__((address_space(3))) const F4v LdsScan;
+template <bool kCount, bool kInst, bool kPerPrimInst>
+__device__ __forceinline__ void lockstep_prims(const LdsScan *P, int first, int count, const float4 *insts,
+                                               const Ray &r, float tmin, bool in, int group_inst, float &best_t,
+                                               int &best_key, uint32_t &best_prim, Counters &cnt) {
+    for (int q = first; q < first + count; ++q) {
+        const F4v g0v = P[4 * q], mmv = P[4 * q + 1];
+        const float4 g0 = f4(g0v);
+        const int kind = __builtin_amdgcn_readfirstlane(fbits(mmv.x)) & 0xff;
+        const int inst = kPerPrimInst ? __builtin_amdgcn_readfirstlane(fbits(mmv.z)) : group_inst;
+        Ray ro = r;
+        if (kInst && kPerPrimInst && inst >= 0) ro = to_object(insts, inst, r);
+        float t;
+        if (kind == RT_PRIM_SPHERE) {
+            t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, ro, tmin);
+        } else if (kind == RT_PRIM_MOVING_SPHERE) {
+            t = sphere_t(msphere_center(g0, f4(P[4 * q + 2]), f4(P[4 * q + 3]), ro.time), g0.w, ro, tmin);
+        } else {
+            t = rect_t(kind, g0, mmv.y, ro, tmin);
+        }
+        const int order = fbits(mmv.w);
+        const int key = kind <= RT_PRIM_MOVING_SPHERE ? order : -1 - order;
+        if (kCount && in) cnt.prim(kind | (kInst && inst >= 0 ? 0x100 : 0));
+        if (kCount && first_active()) cnt.w_prims++;
+        if (in && (t < best_t || (t == best_t && key < best_key))) {
+            best_t = t; best_key = key; best_prim = (uint32_t)q;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ media
 // constant_medium::hit for every medium after the surface search
 // (constant_medium.h:26-50): the boundary's entry/exit, clipped to [t_min, best]

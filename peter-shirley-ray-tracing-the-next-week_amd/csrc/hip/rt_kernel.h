@@ -19,7 +19,8 @@
 #define RT_FEAT_INST 1      // translate / rotate_y / flip_normals chains
 #define RT_FEAT_UV 2        // a material reads (u, v): image_texture
 #define RT_FEAT_CHECKER 4   // checker_texture
-#define RT_FEAT_ALL 7
+#define RT_FEAT_PRESCAN 8   // BVH scene with pre-scanned primitives (RtKernelArgs.nprescan > 0)
+#define RT_FEAT_ALL 15
 
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)
@@ -44,6 +45,7 @@ struct RtKernelArgs {
     int ngroups;
     int scan;               // 1: flat scan of the groups instead of a BVH (small scenes, rt_layout.h)
     uint32_t nprims;        // surface primitives (flat scan: all copied to LDS)
+    int nprescan;           // BVH modes: primitives [0, nprescan) are outside the BVH, tested first in lockstep
     int lds_nodes;          // 1: BVH2 nodes copied to LDS (RT_LDS_BLOCK workgroups, one per CU)
     int stack_depth;        // traversal stack entries per lane of the LDS variant (BVH depth + 1)
     // camera (camera.h members)

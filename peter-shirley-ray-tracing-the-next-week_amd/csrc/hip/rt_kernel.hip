@@ -69,11 +69,12 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 template <bool kCount, bool kProf, int kWidth, int kFeat, int kMode>
 __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     constexpr bool kInst = (kFeat & RT_FEAT_INST) != 0, kUV = (kFeat & RT_FEAT_UV) != 0,
-                   kChecker = (kFeat & RT_FEAT_CHECKER) != 0;
+                   kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
     __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : RT_STACK_DEPTH][64];
-    __shared__ float4 lds_scan[kScan ? 7 * RT_SCAN_MAX : 1];   // kScan: 4 float4 per primitive, 3 per group
+    // kScan: 4 float4 per primitive, 3 per group; BVH modes: the pre-scanned primitives
+    __shared__ float4 lds_scan[kScan ? 7 * RT_SCAN_MAX : (kPrescan ? 4 * RT_PRESCAN_MAX : 1)];
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ CamV4 lds_cam[6];
@@ -96,6 +97,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             lds_dyn[i + 3 * RT_LDS_NODE_CAP] = cf;
         }
     }
+    if (kPrescan && !kScan)
+        for (int i = threadIdx.x; i < 4 * A.nprescan; i += kBlock) lds_scan[i] = A.prims[i];
     if (kScan) {
         for (int i = threadIdx.x; i < 4 * (int)A.nprims; i += kBlock) lds_scan[i] = A.prims[i];
         for (int i = threadIdx.x; i < 3 * A.ngroups; i += kBlock) lds_scan[4 * RT_SCAN_MAX + i] = A.groups[i];
@@ -138,7 +141,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
     };
     // a new ray segment: closest-hit search from the root (hitable_list.h:20-32)
+    bool fresh = false;   // a new segment the pre-scan has not seen yet
     auto begin_segment = [&]() {
+        if (kPrescan) fresh = true;
         node = A.root;
         sp = 0;
         best_t = RT_FLT_MAX;
@@ -253,7 +258,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             // object-space transform per group), primitive by primitive in lockstep.
             const bool act = phase == PH_TRAV;
             if (__ballot(act) != 0ull) {
-                typedef __attribute__((address_space(3))) const F4v LdsScan;
                 const LdsScan *P = (const LdsScan *)lds_scan;
                 const LdsScan *G = P + 4 * RT_SCAN_MAX;
                 const Slab sl = make_slab(r, A.tmin);
@@ -269,31 +273,22 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     const int inst = __builtin_amdgcn_readfirstlane(fbits(gh.z));
                     Ray ro = r;
                     if (kInst && inst >= 0) ro = to_object(A.insts, inst, r);
-                    for (int q = first; q < first + count; ++q) {
-                        const F4v g0v = P[4 * q], mmv = P[4 * q + 1];
-                        const float4 g0 = f4(g0v);
-                        const int m0 = __builtin_amdgcn_readfirstlane(fbits(mmv.x));
-                        const int kind = m0 & 0xff;
-                        float t;
-                        if (kind == RT_PRIM_SPHERE) {
-                            t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, ro, A.tmin);
-                        } else if (kind == RT_PRIM_MOVING_SPHERE) {
-                            t = sphere_t(msphere_center(g0, f4(P[4 * q + 2]), f4(P[4 * q + 3]), ro.time), g0.w, ro, A.tmin);
-                        } else {
-                            t = rect_t(kind, g0, mmv.y, ro, A.tmin);
-                        }
-                        const int order = fbits(mmv.w);
-                        const int key = kind <= RT_PRIM_MOVING_SPHERE ? order : -1 - order;
-                        if (kCount && in) cnt.prim(kind | (kInst && inst >= 0 ? 0x100 : 0));
-                        if (kCount && first_active()) cnt.w_prims++;
-                        if (in && (t < best_t || (t == best_t && key < best_key))) {
-                            best_t = t; best_key = key; best_prim = (uint32_t)q;
-                        }
-                    }
+                    lockstep_prims<kCount, kInst, false>(P, first, count, A.insts, ro, A.tmin, in, inst, best_t, best_key,
+                                                         best_prim, cnt);
                 }
                 if (act) phase = PH_READY;
             }
         } else {
+            // pre-scan: the scene's largest primitives (capi.cpp), kept out of the BVH,
+            // tested in lockstep by every lane with a new segment before its descent;
+            // their hits also shorten best_t, which culls more of the BVH
+            if (kPrescan && A.nprescan > 0) {
+                const bool fr = fresh && phase == PH_TRAV;
+                if (__ballot(fr) != 0ull)
+                    lockstep_prims<kCount, kInst, true>((const LdsScan *)lds_scan, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
+                                                        best_t, best_key, best_prim, cnt);
+                fresh = false;
+            }
             for (;;) {
                 if (__ballot(phase == PH_TRAV) == 0ull) break;
                 if (__popcll(__ballot(phase == PH_READY)) >= RT_READY_BATCH) break;
@@ -473,13 +468,15 @@ static hipError_t launch_features(const RtKernelArgs *a, int grid, int mode, hip
     switch (a->features) {
     case 0: return launch_variant<2, 0, kLds>(a, grid, mode, stream);
     case RT_FEAT_INST: return launch_variant<2, RT_FEAT_INST, kLds>(a, grid, mode, stream);
-    case RT_FEAT_CHECKER: return launch_variant<2, RT_FEAT_CHECKER, kLds>(a, grid, mode, stream);
+    case RT_FEAT_CHECKER:
+    case RT_FEAT_CHECKER | RT_FEAT_PRESCAN:
+        return launch_variant<2, RT_FEAT_CHECKER | RT_FEAT_PRESCAN, kLds>(a, grid, mode, stream);
     default: return launch_variant<2, RT_FEAT_ALL, kLds>(a, grid, mode, stream);
     }
 }
 
 // Compiled variants: every feature (any scene), none (final()), instances only
-// (cornell_box, cornell_smoke), checker only (the random scenes), each with the BVH2
+// (cornell_box, cornell_smoke), checker + pre-scan (the random scenes), each with the BVH2
 // in HBM or in LDS; BVH4 always runs the all-feature variant from HBM.
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (a->scan) return launch_features<2>(a, grid, mode, stream);

@@ -145,6 +145,7 @@ struct rt_scene {
     void *nodes = nullptr, *prims = nullptr, *bprims = nullptr, *media = nullptr, *mats = nullptr, *texs = nullptr,
          *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr, *groups = nullptr;
     bool scan = false;            // flat scan of the primitive groups instead of the BVH (small scenes)
+    int nprescan = 0;             // BVH scenes: largest primitives tested in lockstep before the BVH
     int ngroups = 0;
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
@@ -304,11 +305,64 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     HIP_TRY(hipSetDevice(device));
     trace("device check");
 
+    // Pre-scan (BVH scenes): the largest primitives — box area >= RTNW_PRESCAN_AREA
+    // (default 10 %) of the scene box's, at most RT_PRESCAN_MAX — stay out of the BVH
+    // and are tested in lockstep before every descent (rt_kernel.hip): a primitive
+    // whose box spans the scene sits at the BVH's root and nearly every ray tests it
+    // anyway.  random_motion's ground sphere: c3 55.57 -> 52.15 ms; final()'s six
+    // largest (0.5 %: 2-3 % each) 59.08 -> 62.27 ms, so the threshold leaves them in
+    // the BVH.  RTNW_PRESCAN=0 keeps every primitive in the BVH.
+    std::vector<int> big, rest;
+    {
+        bool want = d->nprims > RT_SCAN_MAX;
+        if (const char *e = std::getenv("RTNW_PRESCAN")) want = want && std::atoi(e) != 0;
+        double frac = 0.10;
+        if (const char *e = std::getenv("RTNW_PRESCAN_AREA")) frac = std::atof(e);
+        std::vector<double> area(d->nprims, 0.0);
+        if (want) {
+            double slo[3] = {1e300, 1e300, 1e300}, shi[3] = {-1e300, -1e300, -1e300};
+            for (int i = 0; i < d->nprims; i++) {
+                float lo[3], hi[3];
+                rtnw::prim_bounds(d->prims[i], d->instances, d->time0, d->time1, lo, hi);
+                for (int k = 0; k < 3; k++) { slo[k] = std::min(slo[k], (double)lo[k]); shi[k] = std::max(shi[k], (double)hi[k]); }
+                const double x = (double)hi[0] - lo[0], y = (double)hi[1] - lo[1], z = (double)hi[2] - lo[2];
+                area[i] = 2 * (x * y + y * z + z * x);
+            }
+            const double x = shi[0] - slo[0], y = shi[1] - slo[1], z = shi[2] - slo[2];
+            const double sa = 2 * (x * y + y * z + z * x);
+            std::vector<int> cand;
+            for (int i = 0; i < d->nprims; i++) if (area[i] >= frac * sa) cand.push_back(i);
+            std::stable_sort(cand.begin(), cand.end(), [&](int p, int q) { return area[p] > area[q]; });
+            if ((int)cand.size() > RT_PRESCAN_MAX) cand.resize(RT_PRESCAN_MAX);
+            std::sort(cand.begin(), cand.end());
+            big = cand;
+        }
+        std::vector<char> is_big(d->nprims, 0);
+        for (int i : big) is_big[i] = 1;
+        for (int i = 0; i < d->nprims; i++) if (!is_big[i]) rest.push_back(i);
+    }
+    std::vector<rt_prim> rest_prims;
+    rest_prims.reserve(rest.size());
+    for (int i : rest) rest_prims.push_back(d->prims[i]);
+
     rtnw::BvhResult bvh;
     try {
-        bvh = rtnw::build_bvh(d->prims, d->nprims, d->instances, d->time0, d->time1);
+        bvh = rtnw::build_bvh(rest_prims.data(), (int)rest_prims.size(), d->instances, d->time0, d->time1);
     } catch (const std::exception &ex) {
         return fail(RT_ERR_INVALID, std::string("BVH build failed: ") + ex.what());
+    }
+    // leaf order -> input primitive, the pre-scanned ones first; leaf refs shifted past them
+    for (int &o : bvh.order) o = rest[o];
+    if (!big.empty()) {
+        const uint32_t K = (uint32_t)big.size();
+        auto shift = [&](uint32_t &ref) {
+            if (ref != RT_EMPTY_CHILD && (ref & RT_LEAF_BIT))
+                ref = RT_LEAF_REF(RT_LEAF_FIRST(ref) + K, RT_LEAF_COUNT(ref));
+        };
+        for (auto &n : bvh.nodes2) for (int c = 0; c < 2; c++) shift(n.ch[c]);
+        for (auto &n : bvh.nodes4) for (int c = 0; c < 4; c++) shift(n.ch[c]);
+        shift(bvh.root);
+        bvh.order.insert(bvh.order.begin(), big.begin(), big.end());
     }
     trace("BVH build");
 
@@ -460,6 +514,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->nprims = d->nprims;
     s->ninstances = d->ninstances;
     s->ngroups = (int)groups.size();
+    s->nprescan = s->scan ? 0 : (int)big.size();
 
     if ((e = hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return cleanup(hip_fail(e, "hipDeviceGetAttribute"));
@@ -621,10 +676,11 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.scan = s->scan ? 1 : 0;
     a.groups = (const float4 *)s->groups;
     a.ngroups = s->ngroups;
+    a.nprescan = s->nprescan;
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
-                 (s->has_checker ? RT_FEAT_CHECKER : 0);
+                 (s->has_checker ? RT_FEAT_CHECKER : 0) | (s->nprescan > 0 ? RT_FEAT_PRESCAN : 0);
     for (int k = 0; k < 3; k++) {
         a.org[k] = cam->origin[k];
         a.llc[k] = cam->lower_left_corner[k];
@@ -730,6 +786,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         stats->grid = (double)s->grid[mode];
         stats->lds_level = s->lds_nodes ? 1.0 : 0.0;
         stats->scan_groups = s->scan ? (double)s->ngroups : 0.0;
+        stats->prescan = (double)s->nprescan;
         stats->stack_depth = (double)(s->lds_nodes ? s->stack_depth : RT_STACK_DEPTH);
     }
     return RT_OK;

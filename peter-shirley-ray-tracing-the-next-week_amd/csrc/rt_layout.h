@@ -75,6 +75,8 @@ struct rt_dprim {
 // ONCE, and tests the group's primitives in lockstep (every lane the same one):
 // the instance level of a two-level structure, without per-leaf transforms.
 #define RT_SCAN_MAX 64
+// BVH scenes: at most this many of the largest primitives are pre-scanned (capi.cpp).
+#define RT_PRESCAN_MAX 8
 struct rt_dgroup {
     int32_t first, count, instance, pad;
     float bx[4], bz[4];

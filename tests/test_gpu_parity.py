@@ -376,13 +376,20 @@ def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     cam = rtnw.Camera.preset(cam_name, nx, ny)
     p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, chunk=4, seed=11)
     out, how = {}, {}
+    big = scene == "random_motion"   # its ground sphere spans the scene: pre-scanned (final(): none reach 10 %)
     for width, lds, scan in (("2", "1", "1"), ("2", "1", "0"), ("2", "0", "0"), ("4", "1", "1")):
         monkeypatch.setenv("RTNW_BVH_WIDTH", width)
         monkeypatch.setenv("RTNW_LDS_BVH", lds)
         monkeypatch.setenv("RTNW_SCAN", scan)
+        # the HBM BVH2 keeps every primitive in the tree; the others pre-scan the largest
+        monkeypatch.setenv("RTNW_PRESCAN", "0" if lds == "0" else "1")
         sc = rtnw.Scene.builtin(scene, earth_png=O.EARTH_PNG)   # fixed when the scene is built
         img, st = sc.render_tile(cam, p, 0, 0, nx, ny, stats=True)
         out[width, lds, scan], how[width, lds, scan] = img, (st["lds_level"], st["scan_groups"] > 0)
+        if lds == "0" or not big:
+            assert st["prescan"] == 0
+        else:
+            assert 1 <= st["prescan"] <= 8, st["prescan"]
     small = scene != "final" and scene != "random_motion"       # <= 64 primitives: scanned by default
     has_nodes = scene not in ("edge_empty", "edge_single", "earth")   # earth: one sphere, the root is a leaf
     nonempty = scene != "edge_empty"
