@@ -16,6 +16,10 @@
 
 namespace {
 
+// Wave ballot of a bool: the lane mask itself (HIP's __ballot takes an int, and the
+// int round trip can materialise the mask as 0/1 per lane and compare it again).
+__device__ __forceinline__ uint64_t wballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
 // ------------------------------------------------------------------ vec3
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float a, float b, float c) { V3 r; r.x = a; r.y = b; r.z = c; return r; }
@@ -333,7 +337,7 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
 // Closest boundary hit of a constant_medium (its own small list), t > / >= tmin.
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask);
 // true on exactly one active lane: counts a wave-level event once per wave
-__device__ __forceinline__ bool first_active() { return lanes_below(__ballot(1)) == 0; }
+__device__ __forceinline__ bool first_active() { return lanes_below(wballot(1)) == 0; }
 
 struct Counters {
     uint64_t samples = 0, segments = 0, nodes = 0, spheres = 0, mspheres = 0, rects = 0, instanced = 0, media = 0,
@@ -606,7 +610,7 @@ __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, 
             const uint32_t top = stk[(sp > 0 ? sp : 0) * 64];
             node = pop ? top : node;
         }
-        if (__popcll(__ballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD)) <= kTail) return pleaf;
+        if (__popcll(wballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD)) <= kTail) return pleaf;
     }
 }
 
@@ -680,7 +684,7 @@ template <int K, bool kCount, class Cand>
 __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt, Cand cand) {
     V3 res = mk(0, 0, 0);
     bool pending = want;
-    uint64_t U = __ballot(pending);
+    uint64_t U = wballot(pending);
     while (U != 0ull) {
         const uint32_t m = (uint32_t)__popcll(U);            // wave-uniform
         const uint32_t inv = kCoop.inv[m];
@@ -694,7 +698,7 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
         const uint32_t slot = lane - t * m;
         const uint64_t base = slots[slot].ctr + (uint64_t)(K * t) * kGamma;
         V3 p;
-        const uint64_t okm = __ballot(cand(base, p));
+        const uint64_t okm = wballot(cand(base, p));
         if (kCount && first_active()) cnt.w_rius++;
         uint32_t src = lane;
         bool won = false;
@@ -713,7 +717,7 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
         if (won) res = mk(px, py, pz);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        U = __ballot(pending);
+        U = wballot(pending);
     }
     return res;
 }
@@ -733,7 +737,7 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
     V3 res = mk(0, 0, 0);
     bool pending = want;
     const uint32_t K = disk ? 2u : 3u;
-    uint64_t U = __ballot(pending);
+    uint64_t U = wballot(pending);
     while (U != 0ull) {
         const uint32_t m = (uint32_t)__popcll(U);            // wave-uniform
         const uint32_t inv = kCoop.inv[m];
@@ -750,7 +754,7 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
         const double x = u48(mix64(base + kGamma)), y = u48(mix64(base + 2 * kGamma)), z = u48(mix64(base + 3 * kGamma));
         const float pz = kk == 3u ? 2.0f * (float)z - 1.0f : 0.0f;
         const V3 p = mk(2.0f * (float)x - 1.0f, 2.0f * (float)y - 1.0f, pz);
-        const uint64_t okm = __ballot((double)dot(p, p) < 1.0);
+        const uint64_t okm = wballot((double)dot(p, p) < 1.0);
         if (kCount && first_active()) cnt.w_rius++;
         uint32_t src = lane;
         bool won = false;
@@ -767,7 +771,7 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
         if (won) res = mk(qx, qy, qz);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        U = __ballot(pending);
+        U = wballot(pending);
     }
     return res;
 }
@@ -782,7 +786,7 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
 // Must be called with all 64 lanes of the wave active.
 __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec, const int *perm, CoopSlot *slots,
                                            uint32_t lane) {
-    const uint64_t U = __ballot(want);
+    const uint64_t U = wballot(want);
     if (U == 0ull) return 0.f;
     float res = 0.f;
     const uint32_t m = (uint32_t)__popcll(U);
@@ -930,7 +934,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
         float cc = dot(oc, oc) - sg.w * sg.w;
         float disc = b * b - a * cc;
         const bool valid = disc > 0;
-        if (__ballot(valid) == 0ull) return;   // the whole wave misses the boundary
+        if (wballot(valid) == 0ull) return;   // the whole wave misses the boundary
         const float sq = sqrtf(disc);
         const float ta = (-b - sq) / a;
         const float tb = (-b + sq) / a;
@@ -944,7 +948,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     } else {
         r1 = boundary_t<kCount, kInst>(A.bprims, A.insts, md.x, md.y, r, -RT_FLT_MAX, cnt);
         ok = r1 != RT_INF;
-        if (__ballot(ok) == 0ull) return;
+        if (wballot(ok) == 0ull) return;
         r2 = boundary_t<kCount, kInst>(A.bprims, A.insts, md.x, md.y, r, (float)((double)r1 + 0.0001), cnt);
         ok = ok && r2 != RT_INF;
     }
@@ -952,7 +956,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     r1 = r1 < A.tmin ? A.tmin : r1;
     r2 = r2 > tmax ? tmax : r2;
     ok = ok && !(r1 >= r2);
-    if (__ballot(ok) == 0ull) return;   // no lane inside the medium: no free-flight draw
+    if (wballot(ok) == 0ull) return;   // no lane inside the medium: no free-flight draw
     r1 = r1 < 0 ? 0.f : r1;
     const float distance_inside_boundary = (r2 - r1) * dlen;
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side

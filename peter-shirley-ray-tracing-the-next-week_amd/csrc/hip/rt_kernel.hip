@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             item = 0xFFFFFFFFu;
         }
         bool need = phase == PH_IDLE && !finished && item == 0xFFFFFFFFu;
-        uint64_t need_mask = __ballot(need);
+        uint64_t need_mask = wballot(need);
         while (need_mask != 0ull && !exhausted) {
             if (pool_next == pool_end) {
                 uint32_t base = 0;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             }
             uint32_t wanted = (uint32_t)__popcll(need_mask);
             pool_next += min(wanted, avail);
-            need_mask = __ballot(need);
+            need_mask = wballot(need);
         }
         if (need) finished = true;
     };
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // cooperative rounds: a metal's absorbed reflection; the others start their
         // next sample inside stage 5)
         retire_and_claim();
-        if (__ballot(!finished) == 0ull) break;
+        if (wballot(!finished) == 0ull) break;
         {
             const bool starting = phase == PH_IDLE && !finished;
             float cu_ = 0, cv_ = 0;
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             // group by group (box test for all lanes, skipped when none hits; one
             // object-space transform per group), primitive by primitive in lockstep.
             const bool act = phase == PH_TRAV;
-            if (__ballot(act) != 0ull) {
+            if (wballot(act) != 0ull) {
                 const LdsScan *P = (const LdsScan *)lds_scan;
                 const LdsScan *G = P + 4 * RT_SCAN_MAX;
                 const Slab sl = make_slab(r, A.tmin);
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     box_span(sl, F2{bx.x, bx.y}, F2{bx.z, bx.w}, F2{bz.x, bz.y}, best_t, tn, tf);
                     const bool in = act && tn <= tf;
                     if (kCount && act) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
-                    if (__ballot(in) == 0ull) continue;
+                    if (wballot(in) == 0ull) continue;
                     const int first = __builtin_amdgcn_readfirstlane(fbits(gh.x));
                     const int count = __builtin_amdgcn_readfirstlane(fbits(gh.y));
                     const int inst = __builtin_amdgcn_readfirstlane(fbits(gh.z));
@@ -284,14 +284,14 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             // their hits also shorten best_t, which culls more of the BVH
             if (kPrescan && A.nprescan > 0) {
                 const bool fr = fresh && phase == PH_TRAV;
-                if (__ballot(fr) != 0ull)
+                if (wballot(fr) != 0ull)
                     lockstep_prims<kCount, kInst, true>((const LdsScan *)lds_scan, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
                                                         best_t, best_key, best_prim, cnt);
                 fresh = false;
             }
             for (;;) {
-                if (__ballot(phase == PH_TRAV) == 0ull) break;
-                if (__popcll(__ballot(phase == PH_READY)) >= RT_READY_BATCH) break;
+                if (wballot(phase == PH_TRAV) == 0ull) break;
+                if (__popcll(wballot(phase == PH_READY)) >= RT_READY_BATCH) break;
                 if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
                     const Slab sl = make_slab(r, A.tmin);
