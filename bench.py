@@ -173,11 +173,14 @@ def lib_sha16():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def read_profile(workload_key):
-    """The latest committed PMC summary (profiles/r<NN>/traffic.json, tools/pmc_traffic.py
+def read_profile(workload_key, sha=None):
+    """The committed PMC summary (profiles/r<NN>/traffic.json, tools/pmc_traffic.py
     from separate rocprofv3 passes of this workload): HBM bytes and VALU instructions
-    per sample of the timed megakernel, and the library build they were measured on."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "traffic.json")), reverse=True):
+    per sample of the timed megakernel, and the library build they were measured on.
+    The summary of this very build (lib_sha16 == sha) if one is committed, else the
+    latest round's (profile_matches_library then says false)."""
+    found = []
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "**", "traffic.json"), recursive=True)):
         try:
             with open(path) as f:
                 t = json.load(f)
@@ -185,8 +188,11 @@ def read_profile(workload_key):
             continue
         if t.get("config", "c4") == workload_key:
             t["path"] = os.path.relpath(path, ROOT)
-            return t
-    return None
+            found.append(t)
+    if not found:
+        return None
+    same = [t for t in found if sha and t.get("lib_sha16") == sha]
+    return (same or found)[-1]
 
 
 def end_to_end(scene_name, cam, params, nx, ny, dev):
@@ -313,8 +319,8 @@ def main():
                             flags=rtnw.RT_FLAG_COUNT)
     cst = scene.render_tiles(cam, cnt, tiles, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream, stats=True)
     cache_bytes = cst["algorithmic_bytes"]
-    prof = read_profile("c4" if cfg in ("c4", "c5") and scene_name == "final" else cfg)
     sha = lib_sha16()
+    prof = read_profile("c4" if cfg in ("c4", "c5") and scene_name == "final" else cfg, sha)
     roof = {"bound": "valu_issue", "achieved": None, "peak": VALU_PEAK / 1e9, "unit": "G wave-VALU-instr/s",
             "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
             "lds_level": int(st["lds_level"]), "stack_depth": int(st["stack_depth"]), "scan_groups": int(st["scan_groups"]), "prescan": int(st["prescan"]),
