@@ -35,6 +35,35 @@ __device__ __forceinline__ V3 unit(V3 v) { return divs(v, len(v)); }
 __device__ __forceinline__ float comp(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 
 struct Ray { V3 o, d; float time; };
+
+// x / b, correctly rounded, from y = RN(1/b) (Markstein): q = RN(x*y); the remainder
+// x - b*q is exact as one FMA, and RN(q + r*y) = RN(x / b) whenever y is a normal
+// float and the quotient neither overflows nor underflows (tests/native/div_rn_check.c
+// compares it with IEEE division on 4e8 random pairs).  3 VALU instead of the ~11 of
+// an IEEE division; callers take it only when every lane's y is normal (a wave-uniform
+// test) and their quotients are O(1) (unit vectors, normals, image coordinates) or
+// ray distances, else the IEEE division.
+__device__ __forceinline__ float div_rn(float x, float b, float y) {
+    const float q = x * y;
+    return __builtin_fmaf(__builtin_fmaf(-q, b, x), y, q);
+}
+__device__ __forceinline__ V3 divs_rn(V3 v, float t, float y) { return mk(div_rn(v.x, t, y), div_rn(v.y, t, y), div_rn(v.z, t, y)); }
+__device__ __forceinline__ bool normal_recip(float y) {
+    const float m = __builtin_fabsf(y);
+    return m >= 0x1p-126f && m <= 0x1.fffffep+127f;
+}
+// A divisor shared by several divisions of a lane: a, y = RN(1/a) (one IEEE division),
+// and whether the wave may divide by it with div_rn (every lane that uses it has a
+// normal reciprocal).
+struct Recip { float a, y; bool ok; };
+__device__ __forceinline__ Recip recip_of(float a, bool use) {
+    Recip r;
+    r.a = a;
+    r.y = 1.0f / a;
+    r.ok = wballot(use && !normal_recip(r.y)) == 0ull;
+    return r;
+}
+__device__ __forceinline__ float div_by(float x, const Recip &r) { return r.ok ? div_rn(x, r.a, r.y) : x / r.a; }
 __device__ __forceinline__ V3 at(const Ray &r, float t) { return add(r.o, scale(t, r.d)); }
 
 // ------------------------------------------------------------------- RNG
@@ -305,10 +334,15 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
     if (kInst && inst >= 0) r = to_object(insts, inst, r0);
     Hit h;
     h.p = at(r, t);
+    // sphere normals (p - c) / radius (sphere.h:37, 105): mm.y = RN(1/radius) from the
+    // host (0 when not a normal float: then every lane of the wave divides exactly)
+    const bool rn = wballot(kind <= RT_PRIM_MOVING_SPHERE && mm.y == 0.f) == 0ull;
     if (kind == RT_PRIM_SPHERE) {
-        h.n = divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w);
+        const V3 v = sub(h.p, mk(g0.x, g0.y, g0.z));
+        h.n = rn ? divs_rn(v, g0.w, mm.y) : divs(v, g0.w);
     } else if (kind == RT_PRIM_MOVING_SPHERE) {
-        h.n = divs(sub(h.p, msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time)), g0.w);
+        const V3 v = sub(h.p, msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time));
+        h.n = rn ? divs_rn(v, g0.w, mm.y) : divs(v, g0.w);
     } else {
         int axis = rect_axis(kind);
         h.n = mk(axis == 0 ? 1.f : 0.f, axis == 1 ? 1.f : 0.f, axis == 2 ? 1.f : 0.f);
@@ -318,7 +352,7 @@ __device__ __forceinline__ Hit prim_record(const float4 *P, const float4 *insts,
     h.mat = fbits(mm.x) >> 9;
     if (kUV && (fbits(mats[h.mat * 2 + 1].w) & 1)) {
         if (kind == RT_PRIM_SPHERE) {
-            sphere_uv(divs(sub(h.p, mk(g0.x, g0.y, g0.z)), g0.w), h.u, h.v);   // sphere.h:36
+            sphere_uv(h.n, h.u, h.v);   // sphere.h:36: the same (p - center) / radius, before any flip
         } else if (kind != RT_PRIM_MOVING_SPHERE) {                          // aarect.h:54-59
             float oi, di, oj, dj;
             if (kind == RT_PRIM_XY_RECT) { oi = r.o.x; di = r.d.x; oj = r.o.y; dj = r.d.y; }
@@ -917,8 +951,10 @@ __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds
 
 // One medium's test (constant_medium.h:26-50) against the surface result.
 template <bool kCount, bool kInst = true>
-__device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, float dlen, int depth,
-                                           const Rng &g, bool &have, float &best_t, int &med_mat, Counters &cnt) {
+__device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, const Recip &rd,
+                                           const Recip &ra, int depth, const Rng &g, bool &have, float &best_t,
+                                           int &med_mat, Counters &cnt) {
+    const float dlen = rd.a;
     if (kCount) cnt.media++;
     const int4 md = M.md;
     float r1, r2;
@@ -929,15 +965,15 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
         if (kCount) cnt.spheres++;
         const float4 sg = M.g0;
         V3 oc = sub(r.o, mk(sg.x, sg.y, sg.z));
-        float a = dot(r.d, r.d);
+        const float a = ra.a;
         float b = dot(oc, r.d);
         float cc = dot(oc, oc) - sg.w * sg.w;
         float disc = b * b - a * cc;
         const bool valid = disc > 0;
         if (wballot(valid) == 0ull) return;   // the whole wave misses the boundary
         const float sq = sqrtf(disc);
-        const float ta = (-b - sq) / a;
-        const float tb = (-b + sq) / a;
+        const float ta = div_by(-b - sq, ra);
+        const float tb = div_by(-b + sq, ra);
         // selects, not branches: sphere.h:33-44 for t_min = -FLT_MAX, then t_min = r1 + 0.0001
         const bool fa = ta < RT_FLT_MAX && ta > -RT_FLT_MAX, fb = tb < RT_FLT_MAX && tb > -RT_FLT_MAX;
         r1 = fa ? ta : tb;
@@ -962,7 +998,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
     const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k)));
     const bool hit = ok && hit_distance < distance_inside_boundary;
-    const float tm = r1 + hit_distance / dlen;
+    const float tm = r1 + div_by(hit_distance, rd);
     best_t = hit ? tm : best_t;
     have = have || hit;
     med_mat = hit ? md.w : med_mat;
@@ -973,8 +1009,10 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
 // choosing per medium between the two made the compiler select the address and
 // issue generic (flat) loads, which wait on both memory counters.
 template <bool kCount, bool kInst = true>
-__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, float dlen, int depth,
-                                         const Rng &g, bool &have, float &best_t, Counters &cnt) {
+__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, const Recip &rd,
+                                         int depth, const Rng &g, bool &have, float &best_t, Counters &cnt) {
+    // a = |d|^2 of the boundary spheres' quadratics (sphere.h:28), its reciprocal once for all media
+    const Recip ra = recip_of(dot(r.d, r.d), true);
     typedef unsigned U4v __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) const U4v LdsU4;
     int med_mat = -1;
@@ -986,14 +1024,14 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
         M.md = make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
         M.g0 = make_float4(__uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w));
         M.mm = make_float4(__uint_as_float(z.x), __uint_as_float(z.y), __uint_as_float(z.z), __uint_as_float(z.w));
-        medium_one<kCount, kInst>(A, M, k, r, dlen, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, cnt);
     }
     for (int k = RT_LDS_MEDIA; k < A.nmedia; ++k) {
         MediumRec M;
         M.md = A.media[k];
         M.g0 = A.bprims[M.md.x * 4 + 0];
         M.mm = A.bprims[M.md.x * 4 + 1];
-        medium_one<kCount, kInst>(A, M, k, r, dlen, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, cnt);
     }
     return med_mat;
 }
@@ -1060,11 +1098,11 @@ __device__ __forceinline__ bool shade_ends(bool ready, bool have, const ShadeSta
 
 // emitted() of the segment: the background on a miss (TNW/Chapter03:29-31 for the
 // sky), the light's texture, else black.
-__device__ __forceinline__ V3 shade_emitted(const RtKernelArgs &A, bool have, const Ray &r, float dlen,
+__device__ __forceinline__ V3 shade_emitted(const RtKernelArgs &A, bool have, const Ray &r, const Recip &rd,
                                             const ShadeState &st) {
     if (!have) {
         if (A.background != RT_BG_SKY) return mk(0, 0, 0);
-        const V3 ud = divs(r.d, dlen);   // unit(r.d), vec3.h:146
+        const V3 ud = mk(div_by(r.d.x, rd), div_by(r.d.y, rd), div_by(r.d.z, rd));   // unit(r.d), vec3.h:146
         const float t = (float)(0.5 * ((double)ud.y + 1.0));
         return add(scale((float)(1.0 - (double)t), mk(1.0f, 1.0f, 1.0f)), scale(t, mk(0.5f, 0.7f, 1.0f)));
     }
@@ -1073,7 +1111,7 @@ __device__ __forceinline__ V3 shade_emitted(const RtKernelArgs &A, bool have, co
 
 // material::scatter (material.h) given the lane's random_in_unit_sphere point.
 // dlen = |r.d|, computed once per segment and shared with the media (RtKernelArgs.need_dlen).
-__device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool ready, bool have, const Ray &r, float dlen,
+__device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool ready, bool have, const Ray &r, const Recip &rd,
                                                  const Hit &hr, const ShadeState &st, V3 rius, Rng &g) {
     ShadeOut o;
     o.scattered = false;
@@ -1085,9 +1123,9 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
     // dielectric) instead of once in each of their branches
     const bool wants_unit = ready && have && st.live && (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC);
     V3 ud = mk(0, 0, 0);
-    if (wants_unit) ud = divs(r.d, dlen);
+    if (wants_unit) ud = mk(div_by(r.d.x, rd), div_by(r.d.y, rd), div_by(r.d.z, rd));
     if (!ready) return o;
-    o.emitted = shade_emitted(A, have, r, dlen, st);
+    o.emitted = shade_emitted(A, have, r, rd, st);
     if (!have || !st.live) return o;
     const float4 m0 = A.mats[hr.mat * 2 + 0];
     const float4 m1 = A.mats[hr.mat * 2 + 1];
@@ -1112,12 +1150,12 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
         if (dn > 0) {
             outward_normal = neg(hr.n);
             ni_over_nt = ref_idx;
-            cosine = dot(r.d, hr.n) / dlen;
+            cosine = div_by(dot(r.d, hr.n), rd);
             cosine = sqrtf(1 - m1.z * (1 - cosine * cosine));   // m1.z = ref_idx * ref_idx
         } else {
             outward_normal = hr.n;
             ni_over_nt = m1.x;                                   // (float)(1.0 / (double)ref_idx)
-            cosine = -dot(r.d, hr.n) / dlen;
+            cosine = div_by(-dot(r.d, hr.n), rd);
         }
         // refract, material.h:23-33
         const V3 uv = ud;
@@ -1143,22 +1181,6 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
     }
     o.ray = ns;
     return o;
-}
-
-// color() at one hit (main.cpp:27-45) and material::scatter (material.h).
-// Lanes with `ready` false only help the cooperative samplers.  The per-material
-// work that dominates (texture lookup, the rejection loop of
-// random_in_unit_sphere) runs ONCE for every lane that needs it instead of once
-// per material branch; each lane still makes exactly the draws its own material
-// makes, in the same order (one material per lane).  No hit: `emitted` is the
-// background.  Must be called with all 64 lanes of the wave active.
-template <bool kCount, bool kUV = true, bool kChecker = true>
-__device__ __forceinline__ ShadeOut shade(const RtKernelArgs &A, bool ready, bool have, const Ray &r, float dlen,
-                                          const Hit &hr, int depth, Rng &g, CoopSlot *slots, uint32_t lane,
-                                          Counters &cnt) {
-    const ShadeState st = shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt);
-    const V3 rius = coop_reject<3, kCount>(st.wants_sphere, g, slots, lane, cnt, SphereCand());   // material.h:41-47
-    return shade_finish(A, ready, have, r, dlen, hr, st, rius, g);
 }
 
 }  // namespace

@@ -53,6 +53,7 @@ struct RtKernelArgs {
     float lens, ct0, ct1;
     // render parameters
     int nx, ny, ns, max_depth;
+    float rnx, rny;           // RN(1/float(nx)), RN(1/float(ny)): the camera's divisions by div_rn
     float tmin;
     int background;
     int chunk, nchunks;       // samples per work item; work items per pixel in this launch

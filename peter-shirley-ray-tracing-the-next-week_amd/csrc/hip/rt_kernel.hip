@@ -197,8 +197,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (starting) {
             int j = A.ny - 1 - (int)py;
             g.start(sample_key(skey, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
-            cu_ = (float)((double)(int)px + g.next()) / (float)A.nx;
-            cv_ = (float)((double)j + g.next()) / (float)A.ny;
+            // main.cpp:305-306; A.rnx = RN(1/float(nx)) from the host (div_rn)
+            cu_ = div_rn((float)((double)(int)px + g.next()), (float)A.nx, A.rnx);
+            cv_ = div_rn((float)((double)j + g.next()), (float)A.ny, A.rny);
         }
     };
     auto camera_finish = [&](bool starting, float cu_, float cv_, V3 disk) {
@@ -337,11 +338,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         bool have = false;
         // |r.d| once per segment, for the media and the specular materials / sky
         const float dlen = (ready && A.need_dlen) ? len(r.d) : 0.f;
+        const Recip rd = recip_of(dlen, ready && A.need_dlen);   // its reciprocal, for div_rn
         Hit hr;
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            const int med_mat = media_hit<kCount, kInst>(A, lds_media, r, dlen, depth, g, have, best_t, cnt);
+            const int med_mat = media_hit<kCount, kInst>(A, lds_media, r, rd, depth, g, have, best_t, cnt);
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // in the same cooperative rounds as the scattering lanes' sphere candidates.
         const ShadeState st = shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt);
         const bool ends = shade_ends(ready, have, st);
-        if (ends) end_path(mul(beta, shade_emitted(A, have, r, dlen, st)));
+        if (ends) end_path(mul(beta, shade_emitted(A, have, r, rd, st)));
         retire_and_claim();
         const bool starting = phase == PH_IDLE && !finished;
         float cu_ = 0, cv_ = 0;
@@ -367,7 +369,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
         const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, lane, cnt);
         if (ready && !ends) {
-            const ShadeOut so = shade_finish(A, ready, have, r, dlen, hr, st, pt, g);
+            const ShadeOut so = shade_finish(A, ready, have, r, rd, hr, st, pt, g);
             if (so.scattered) {
                 beta = mul(beta, so.att);
                 r = so.ray;

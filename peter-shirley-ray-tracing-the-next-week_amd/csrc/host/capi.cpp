@@ -107,7 +107,12 @@ rt_dprim to_dprim(const rt_prim &p, int order) {
         break;
     }
     d.m[0] = p.kind | (p.flip ? 1 << 8 : 0) | (p.material << 9);
-    d.m[1] = p.kind >= RT_PRIM_XY_RECT ? ibits(q[4]) : 0;   // rect plane k
+    if (p.kind >= RT_PRIM_XY_RECT) {
+        d.m[1] = ibits(q[4]);   // rect plane k
+    } else {                    // spheres: RN(1/radius) for the normal's div_rn, 0 if not a normal float
+        const float y = 1.0f / d.g0[3];
+        d.m[1] = (std::isnormal(y)) ? ibits(y) : 0;
+    }
     d.m[2] = p.instance;
     d.m[3] = order;
     return d;
@@ -694,6 +699,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.ct1 = cam->time1;
     a.nx = p->nx;
     a.ny = p->ny;
+    a.rnx = 1.0f / (float)p->nx;   // nx, ny >= 1: normal reciprocals (div_rn, rt_device.h)
+    a.rny = 1.0f / (float)p->ny;
     a.ns = p->spp;
     a.max_depth = p->max_depth;
     a.tmin = p->t_min;

@@ -231,3 +231,15 @@ def test_checkpoint_round_trip_and_corruption(tmp_path):
         rtnw.read_checkpoint(str(tmp_path / "c.rtck"))
     with pytest.raises(rtnw.RtError):
         rtnw.read_checkpoint(str(tmp_path / "missing.rtck"))
+
+
+def test_shared_reciprocal_division_is_ieee(tmp_path):
+    """tests/native/div_rn_check.c: the kernel's div_rn (Markstein: q = RN(x y),
+    fma(fma(-q, b, x), y, q) with y = RN(1/b)) equals IEEE x / b on 1e8 random
+    divisions of the kernel's shapes (normal reciprocals and quotients)."""
+    exe = str(tmp_path / "div_rn_check")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", os.path.join(ROOT, "tests", "native", "div_rn_check.c"),
+                    "-o", exe, "-lm"], check=True, capture_output=True)
+    out = subprocess.run([exe, "20000000"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.strip().startswith("0 mismatches")
