@@ -70,11 +70,19 @@ __device__ __forceinline__ V3 at(const Ray &r, float t) { return add(r.o, scale(
 // Counter streams: sample (pixel, s) draws u48(mix64(key + n*GAMMA)),
 // n = 1, 2, ...; constant_medium k at bounce b draws from a second keyed stream.
 constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+__device__ __forceinline__ uint64_t mix64_(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
+#ifdef RT_PROBE_MIX
+}  // namespace
+__device__ uint64_t rt_probe_zero;   // timing probe only: a second mix64 per call, masked by a run-time 0
+namespace {
+__device__ __forceinline__ uint64_t mix64(uint64_t z) { return mix64_(z) ^ (mix64_(z ^ 0x1234567ull) & rt_probe_zero); }
+#else
+__device__ __forceinline__ uint64_t mix64(uint64_t z) { return mix64_(z); }
+#endif
 // (z >> 16) * 2^-48, built as the double 1 + (z >> 16) * 2^-48 (the 48 bits as the
 // top of the 52-bit mantissa) minus 1: both steps exact, so the same value as the
 // integer conversion, for one f64 add instead of two conversions, a scale and an add.
@@ -93,6 +101,7 @@ struct Rng {
     uint64_t mkey;   // medium stream key, derived once per sample
     __device__ __forceinline__ void start(uint64_t k) { ctr = k; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
     __device__ __forceinline__ double next() { ctr += kGamma; return u48(mix64(ctr)); }
+    __device__ __forceinline__ void skip() { ctr += kGamma; }   // a draw whose value is not used
     __device__ __forceinline__ double medium(int bounce, int k) const {
         uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
         return u48(mix64(mkey + (m + 1) * kGamma));
@@ -542,6 +551,8 @@ struct GlobalNodes {
         b0 = N[0]; b1 = N[1]; b2 = N[2]; cf = N[3];
     }
     __device__ __forceinline__ const float4 *ptr4(uint32_t n) const { return p + n * 8; }
+    __device__ __forceinline__ const float4 *ptr8(uint32_t n) const { return p + n * 16; }
+    __device__ __forceinline__ const float4 *ptr8q(uint32_t n) const { return p + n * 8; }
 };
 struct LdsNodes {
     const LdsF4 *p;
@@ -549,8 +560,34 @@ struct LdsNodes {
         const LdsF4 *N = p + n;
         b0 = f4(N[0]); b1 = f4(N[RT_LDS_NODE_CAP]); b2 = f4(N[2 * RT_LDS_NODE_CAP]); cf = f4(N[3 * RT_LDS_NODE_CAP]);
     }
-    __device__ __forceinline__ const float4 *ptr4(uint32_t) const { return nullptr; }   // BVH4 stays in HBM
+    __device__ __forceinline__ const float4 *ptr4(uint32_t) const { return nullptr; }   // wide BVHs stay in HBM
+    __device__ __forceinline__ const float4 *ptr8(uint32_t) const { return nullptr; }
+    __device__ __forceinline__ const float4 *ptr8q(uint32_t) const { return nullptr; }
 };
+
+// 8-wide node step's tail: the nearest hit child (the first one in slot order on
+// ties) is the next node, the other hit children are pushed in reverse slot order.
+// The builder puts the children in slots by direction from the node's centre (slot
+// bit a set = the child lies on the + side of axis a), so rays going + on all axes
+// pop the nearer siblings first; siblings are not sorted per ray: an 8-key sort
+// costs more VALU than the box tests themselves.
+__device__ __forceinline__ uint32_t wide8_tail(const float k[8], const uint32_t ch[8], uint32_t *stk, int &sp) {
+    const float kmin = vmin(vmin3(vmin3(k[0], k[1], k[2]), vmin3(k[3], k[4], k[5]), k[6]), k[7]);
+    int sel = 8;   // the first slot holding the nearest hit (8: no hit)
+#pragma unroll
+    for (int c = 7; c >= 0; --c) sel = (k[c] != RT_INF && k[c] == kmin) ? c : sel;
+    uint32_t next = RT_EMPTY_CHILD;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        next = c == sel ? ch[c] : next;
+    }
+#pragma unroll
+    for (int c = 7; c >= 0; --c) {   // slot written, then kept only if pushed
+        stk[sp * 64] = ch[c];
+        sp += (k[c] != RT_INF && c != sel) ? 1 : 0;
+    }
+    return next;
+}
 
 // One interior node: test the children, push the hit ones but the nearest far to
 // near (branch-free: a slot is written, then kept only if the child was hit; the
@@ -576,6 +613,50 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
         const int sp0 = h0 ? sp + 1 : sp;
         sp = h1 ? sp0 : sp;
         return nearc;
+    } else if (kWidth == 8) {   // rt_dnode8
+        const float4 *N = src.ptr8(node);
+        float4 q[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) q[i] = N[i];
+        const float4 c0 = N[12], c1 = N[13];
+        const uint32_t ch[8] = {(uint32_t)fbits(c0.x), (uint32_t)fbits(c0.y), (uint32_t)fbits(c0.z), (uint32_t)fbits(c0.w),
+                                (uint32_t)fbits(c1.x), (uint32_t)fbits(c1.y), (uint32_t)fbits(c1.z), (uint32_t)fbits(c1.w)};
+        float k[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int p = c >> 1;
+            const float4 x = q[p], y = q[4 + p], z = q[8 + p];
+            k[c] = (c & 1) ? box_entry<true>(s, F2{x.z, x.w}, F2{y.z, y.w}, F2{z.z, z.w}, best_t, ch[c])
+                           : box_entry<true>(s, F2{x.x, x.y}, F2{y.x, y.y}, F2{z.x, z.y}, best_t, ch[c]);
+        }
+        return wide8_tail(k, ch, stk, sp);
+    } else if (kWidth == RT_BVH_CW8) {   // rt_dnode8q: planes origin + q * 2^e, in ray space
+        const float4 *N = src.ptr8q(node);
+        const float4 h = N[0], qx = N[1], qy = N[2], qz = N[3], c0 = N[4], c1 = N[5];
+        const uint32_t ch[8] = {(uint32_t)fbits(c0.x), (uint32_t)fbits(c0.y), (uint32_t)fbits(c0.z), (uint32_t)fbits(c0.w),
+                                (uint32_t)fbits(c1.x), (uint32_t)fbits(c1.y), (uint32_t)fbits(c1.z), (uint32_t)fbits(c1.w)};
+        const uint32_t eb = (uint32_t)fbits(h.w);
+        // t(plane q) = (origin + q * step - o) / d = q * (step / d) + (origin - o) / d
+        const float ax = __uint_as_float((eb & 0xFFu) << 23) * s.ix.x, bx = __builtin_fmaf(h.x, s.ix.x, s.nox.x);
+        const float ay = __uint_as_float(((eb >> 8) & 0xFFu) << 23) * s.iy.x, by = __builtin_fmaf(h.y, s.iy.x, s.noy.x);
+        const float az = __uint_as_float(((eb >> 16) & 0xFFu) << 23) * s.iz.x, bz = __builtin_fmaf(h.z, s.iz.x, s.noz.x);
+        const uint32_t wx[4] = {(uint32_t)fbits(qx.x), (uint32_t)fbits(qx.y), (uint32_t)fbits(qx.z), (uint32_t)fbits(qx.w)};
+        const uint32_t wy[4] = {(uint32_t)fbits(qy.x), (uint32_t)fbits(qy.y), (uint32_t)fbits(qy.z), (uint32_t)fbits(qy.w)};
+        const uint32_t wz[4] = {(uint32_t)fbits(qz.x), (uint32_t)fbits(qz.y), (uint32_t)fbits(qz.z), (uint32_t)fbits(qz.w)};
+        float k[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int w = c >> 2, sh = 8 * (c & 3);
+            const F2 px = F2{(float)((wx[w] >> sh) & 0xFFu), (float)((wx[2 + w] >> sh) & 0xFFu)};
+            const F2 py = F2{(float)((wy[w] >> sh) & 0xFFu), (float)((wy[2 + w] >> sh) & 0xFFu)};
+            const F2 pz = F2{(float)((wz[w] >> sh) & 0xFFu), (float)((wz[2 + w] >> sh) & 0xFFu)};
+            const F2 a = pk_fma(px, F2{ax, ax}, F2{bx, bx}), b = pk_fma(py, F2{ay, ay}, F2{by, by}),
+                     e = pk_fma(pz, F2{az, az}, F2{bz, bz});
+            const float tn = imax(vmax3(vmin(a.x, a.y), vmin(b.x, b.y), vmin(e.x, e.y)), s.tmin);
+            const float tf = imin(vmin3(vmax(a.x, a.y), vmax(b.x, b.y), vmax(e.x, e.y)), best_t);
+            k[c] = (tn <= tf && ch[c] != RT_EMPTY_CHILD) ? tn : RT_INF;
+        }
+        return wide8_tail(k, ch, stk, sp);
     } else {             // rt_dnode4
         const float4 *N = src.ptr4(node);
         const float4 qx01 = N[0], qx23 = N[1], qy01 = N[2], qy23 = N[3], qz01 = N[4], qz23 = N[5], cf = N[6];

@@ -24,7 +24,7 @@
 
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)
-    const float4 *nodes;    // BVH nodes, breadth-first: 4 x float4 (width 2) or 8 x float4 (width 4)
+    const float4 *nodes;    // BVH nodes, breadth-first: 4 / 8 / 16 / 8 x float4 (width 2 / 4 / 8 / RT_BVH_CW8)
     const float4 *prims;    // 4 x float4 per surface primitive (leaf order)
     const float4 *bprims;   // 4 x float4 per media-boundary primitive
     const int4 *media;      // 1 x int4 per medium
@@ -36,7 +36,7 @@ struct RtKernelArgs {
     const uint8_t *texels;  // image_texture bytes
     uint32_t root;
     uint32_t nnodes;
-    int bvh_width;          // 2 or 4
+    int bvh_width;          // 2, 4, 8 or RT_BVH_CW8 (compressed 8-wide)
     int has_bvh;
     int nmedia;
     int features;           // RT_FEAT_* present in the scene (selects the megakernel variant)
@@ -78,7 +78,7 @@ extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int 
 #define RT_RESOLVE_RAW 8      // write the sums themselves (checkpoints), not sum * k
 extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
-// mode: 0 plain, 1 count, 2 profile; width: BVH width of the scene (2 or 4), 0: the flat-scan kernel
+// mode: 0 plain, 1 count, 2 profile; width: the scene's RtKernelArgs.bvh_width, 0: the flat-scan kernel
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);
 // Static LDS bytes of the LDS-BVH variant (its dynamic part: nodes + stacks).
 extern "C" int rt_megakernel_lds_static_bytes(void);

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
-    __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : RT_STACK_DEPTH][64];
+    __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : (kWidth >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH)][64];
     // kScan: 4 float4 per primitive, 3 per group; BVH modes: the pre-scanned primitives
     __shared__ float4 lds_scan[kScan ? 7 * RT_SCAN_MAX : (kPrescan ? 4 * RT_PRESCAN_MAX : 1)];
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
@@ -207,7 +207,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const CamView C = load_camera(lds_cam);
             V3 rd = scale(C.lens, disk);
             V3 offset = add(scale(rd.x, C.cu), scale(rd.y, C.cv));
-            float time = (float)((double)C.t0 + g.next() * (double)(C.t1 - C.t0));
+            // camera.h:54: a closed shutter (t1 - t0 == 0, final() and the Cornell scenes)
+            // gives time0 + u*0 = time0 for every draw u, so the draw is consumed unhashed
+            const float span = C.t1 - C.t0;
+            double u = 0.0;
+            if (span != 0.0f) u = g.next(); else g.skip();
+            float time = (float)((double)C.t0 + u * (double)span);
             V3 org = C.org;
             V3 dir = sub(sub(add(add(C.llc, scale(cu_, C.hor)), scale(cv_, C.ver)), org), offset);
             r.o = add(org, offset);
@@ -479,10 +484,12 @@ static hipError_t launch_features(const RtKernelArgs *a, int grid, int mode, hip
 
 // Compiled variants: every feature (any scene), none (final()), instances only
 // (cornell_box, cornell_smoke), checker + pre-scan (the random scenes), each with the BVH2
-// in HBM or in LDS; BVH4 always runs the all-feature variant from HBM.
+// in HBM or in LDS; the wide BVHs (4, 8, compressed 8) run the all-feature variant from HBM.
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (a->scan) return launch_features<2>(a, grid, mode, stream);
     if (a->bvh_width == 4) return launch_variant<4, RT_FEAT_ALL, 0>(a, grid, mode, stream);
+    if (a->bvh_width == 8) return launch_variant<8, RT_FEAT_ALL, 0>(a, grid, mode, stream);
+    if (a->bvh_width == RT_BVH_CW8) return launch_variant<RT_BVH_CW8, RT_FEAT_ALL, 0>(a, grid, mode, stream);
     return a->lds_nodes ? launch_features<1>(a, grid, mode, stream) : launch_features<0>(a, grid, mode, stream);
 }
 
@@ -504,6 +511,8 @@ static hipError_t occupancy_width(int *blocks_per_cu, int mode) {
 
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width) {
     if (width == 0) return occupancy_width<2, 2>(blocks_per_cu, mode);
+    if (width == 8) return occupancy_width<8, 0>(blocks_per_cu, mode);
+    if (width == RT_BVH_CW8) return occupancy_width<RT_BVH_CW8, 0>(blocks_per_cu, mode);
     return width == 4 ? occupancy_width<4, 0>(blocks_per_cu, mode) : occupancy_width<2, 0>(blocks_per_cu, mode);
 }
 

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <cmath>
 #include <stdexcept>
 
@@ -252,6 +253,15 @@ void put_box(rt_dnode4 &n, int c, const Box &b) {
         q[1] = hi[a];
     }
 }
+void put_box(rt_dnode8 &n, int c, const Box &b) {
+    float lo[3], hi[3];
+    float_box(b, lo, hi);
+    for (int a = 0; a < 3; a++) {
+        float *q = n.q[4 * a + (c >> 1)] + 2 * (c & 1);
+        q[0] = lo[a];
+        q[1] = hi[a];
+    }
+}
 void put_box(rt_dnode2 &n, int c, const Box &b) {
     float lo[3], hi[3];
     float_box(b, lo, hi);
@@ -262,7 +272,50 @@ void put_box(rt_dnode2 &n, int c, const Box &b) {
     }
 }
 
-// Emits the binary tree breadth-first, 2-wide as built or collapsed 4-wide: a
+// Compressed BVH8 node from the float boxes of its n children (rt_layout.h
+// rt_dnode8q): the grid of axis a starts at the union's lo (rounded down to float)
+// with the smallest power-of-two step whose 255 steps cover the union; each plane is
+// quantised outward in double, so the decoded box contains the float box.
+rt_dnode8q quantise(const rt_dnode8 &f) {
+    rt_dnode8q q{};
+    for (int c = 0; c < 8; c++) q.ch[c] = f.ch[c];
+    uint32_t ebits = 0;
+    for (int a = 0; a < 3; a++) {
+        double lo = 1e300, hi = -1e300;
+        for (int c = 0; c < 8; c++) {
+            if (f.ch[c] == RT_EMPTY_CHILD) continue;
+            const float *p = f.q[4 * a + (c >> 1)] + 2 * (c & 1);
+            lo = std::min(lo, (double)p[0]);
+            hi = std::max(hi, (double)p[1]);
+        }
+        float org = (float)lo;
+        if ((double)org > lo) org = std::nextafter(org, -INFINITY);
+        int e = -126;   // 2^e, e in [-126, 127]: 255 * 2^e >= hi - org
+        while (e < 127 && std::ldexp(255.0, e) < hi - (double)org) e++;
+        const double step = std::ldexp(1.0, e);
+        q.origin[a] = org;
+        ebits |= (uint32_t)(e + 127) << (8 * a);
+        uint8_t qlo[8], qhi[8];
+        for (int c = 0; c < 8; c++) {
+            if (f.ch[c] == RT_EMPTY_CHILD) { qlo[c] = 0; qhi[c] = 0; continue; }   // empty slot: masked by its reference
+            const float *p = f.q[4 * a + (c >> 1)] + 2 * (c & 1);
+            const double l = std::floor(((double)p[0] - (double)org) / step);
+            const double h = std::ceil(((double)p[1] - (double)org) / step);
+            qlo[c] = (uint8_t)std::max(0.0, std::min(255.0, l));
+            qhi[c] = (uint8_t)std::max(0.0, std::min(255.0, h));
+        }
+        for (int w = 0; w < 2; w++) {
+            q.qa[a][w] = (uint32_t)qlo[4 * w] | (uint32_t)qlo[4 * w + 1] << 8 | (uint32_t)qlo[4 * w + 2] << 16 |
+                         (uint32_t)qlo[4 * w + 3] << 24;
+            q.qa[a][2 + w] = (uint32_t)qhi[4 * w] | (uint32_t)qhi[4 * w + 1] << 8 | (uint32_t)qhi[4 * w + 2] << 16 |
+                             (uint32_t)qhi[4 * w + 3] << 24;
+        }
+    }
+    q.ebits = ebits;
+    return q;
+}
+
+// Emits the binary tree breadth-first, 2-wide as built or collapsed 4- or 8-wide: a
 // node opens its largest-area interior child into that child's two children
 // until it has `width`.  `budget`
 // bounds the traversal stack below the node: a node with n children pushes at
@@ -276,8 +329,8 @@ struct Collapser {
 
     struct Cand { uint32_t ref; Box box; };
 
-    // Children of one 4-wide node (n of them) for binary node `ref`.
-    int expand(uint32_t ref, int budget, Cand cs[4]) const {
+    // Children of one wide node (n of them) for binary node `ref`.
+    int expand(uint32_t ref, int budget, Cand cs[8]) const {
         const Node2 &n2 = b.nodes[ref];
         cs[0] = {n2.ch[0], n2.box[0]};
         cs[1] = {n2.ch[1], n2.box[1]};
@@ -316,9 +369,10 @@ struct Collapser {
         queue.push_back({root, budget, 0});
         for (size_t qi = 0; qi < queue.size(); ++qi) {
             const Job j = queue[qi];
-            Cand cs[4];
+            Cand cs[8];
             const int n = expand(j.ref, j.budget, cs);
-            uint32_t ch[4] = {RT_EMPTY_CHILD, RT_EMPTY_CHILD, RT_EMPTY_CHILD, RT_EMPTY_CHILD};
+            uint32_t ch[8];
+            for (uint32_t &c : ch) c = RT_EMPTY_CHILD;
             for (int i = 0; i < n; i++) {
                 if (cs[i].ref & RT_LEAF_BIT) {
                     ch[i] = cs[i].ref;
@@ -328,9 +382,38 @@ struct Collapser {
                     queue.push_back({cs[i].ref, j.budget - (n - 1), ch[i]});
                 }
             }
+            // 8-wide: slots by direction from the node's centre (slot bit a = + side of
+            // axis a), greedily, so slot order is near-to-far for rays going + on all axes
+            int slot[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+            if (width == 8) {
+                Box all;
+                for (int i = 0; i < n; i++) all.grow(cs[i].box);
+                bool used_c[8] = {}, used_s[8] = {};
+                for (int k = 0; k < n; k++) {
+                    double best = 1e300;
+                    int bc = -1, bs = -1;
+                    for (int i = 0; i < n; i++) {
+                        if (used_c[i]) continue;
+                        for (int sl = 0; sl < 8; sl++) {
+                            if (used_s[sl]) continue;
+                            double cost = 0;
+                            for (int a = 0; a < 3; a++) {
+                                const double d = 0.5 * (cs[i].box.lo[a] + cs[i].box.hi[a]) - 0.5 * (all.lo[a] + all.hi[a]);
+                                cost -= ((sl >> a) & 1) ? d : -d;
+                            }
+                            if (cost < best) { best = cost; bc = i; bs = sl; }
+                        }
+                    }
+                    used_c[bc] = used_s[bs] = true;
+                    slot[bc] = bs;
+                }
+            }
             Node &node = out[j.id];
-            for (int i = 0; i < n; i++) put_box(node, i, cs[i].box);
-            for (int i = 0; i < 4; i++) node.ch[i] = ch[i];
+            for (int i = 0; i < width; i++) node.ch[i] = RT_EMPTY_CHILD;
+            for (int i = 0; i < n; i++) {
+                put_box(node, slot[i], cs[i].box);
+                node.ch[slot[i]] = ch[i];
+            }
         }
         return 0;
     }
@@ -345,6 +428,14 @@ void prim_bounds(const rt_prim &p, const rt_instance *instances, float time0, fl
 
 BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, float time0, float time1) {
     BvhResult res;
+    int width = 2;
+    bool quant = false;
+    if (const char *e = std::getenv("RTNW_BVH_WIDTH")) {
+        const int w = std::atoi(e);
+        width = (w == 4 || w == 8) ? w : 2;
+        quant = width == 8 && std::strchr(e, 'q') != nullptr;
+    }
+    res.width = quant ? RT_BVH_CW8 : width;
     if (n <= 0) return res;
     const double ta = std::min(0.0, (double)time0), tb = std::max(0.0, (double)time1);
     Builder b;
@@ -358,9 +449,6 @@ BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, f
         for (int k = 0; k < 3; k++) it.c[k] = 0.5 * (it.box.lo[k] + it.box.hi[k]);
         it.idx = i;
     }
-    int width = 2;
-    if (const char *e = std::getenv("RTNW_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
-    res.width = width;
     const uint32_t root2 = b.build(0, n, 0);
     auto emit = [&](auto &out_nodes, auto node_tag) {
         using Node = decltype(node_tag);
@@ -376,8 +464,26 @@ BvhResult build_bvh(const rt_prim *prims, int n, const rt_instance *instances, f
         res.root = 0;
         out_nodes = std::move(c.out);
     };
-    if (width == 4) emit(res.nodes4, rt_dnode4{});
-    else emit(res.nodes2, rt_dnode2{});
+    if (width == 4) {
+        emit(res.nodes4, rt_dnode4{});
+    } else if (width == 8) {
+        Collapser<rt_dnode8> c{b, 8, {}};
+        if (root2 & RT_LEAF_BIT) {
+            res.depth = 0;
+            res.root = root2;
+        } else {
+            c.collapse(root2, RT_STACK_DEPTH_W8 - 1);
+            res.depth = b.max_depth_seen;
+            res.root = 0;
+        }
+        if (quant) {
+            for (const rt_dnode8 &nd : c.out) res.nodes8q.push_back(quantise(nd));
+        } else {
+            res.nodes8 = std::move(c.out);
+        }
+    } else {
+        emit(res.nodes2, rt_dnode2{});
+    }
     res.order = std::move(b.order);
     return res;
 }

@@ -74,9 +74,9 @@ int commit(Arena &a, void **base) {
 // property of the code objects, queried once per process.
 hipError_t occupancy(int *mega, int mode, int width) {
     static std::mutex mu;
-    static int cache[3][3] = {};   // [mode][BVH2, BVH4, flat scan]
+    static int cache[3][5] = {};   // [mode][BVH2, BVH4, flat scan, BVH8, compressed BVH8]
     std::lock_guard<std::mutex> lock(mu);
-    int &c = cache[mode][width == 4 ? 1 : (width == 0 ? 2 : 0)];
+    int &c = cache[mode][width == 4 ? 1 : width == 0 ? 2 : width == 8 ? 3 : width == RT_BVH_CW8 ? 4 : 0];
     if (!c) {
         hipError_t e;
         if ((e = rt_megakernel_occupancy(&c, mode, width)) != hipSuccess) { c = 0; return e; }
@@ -120,7 +120,8 @@ rt_dprim to_dprim(const rt_prim &p, int order) {
 
 // SURVEY §8d byte model (bytes the algorithm must read or write, independent of
 // this implementation's record padding):
-//   node fetch: the bytes loaded per visit (BVH2 64 B, BVH4 112 B); sphere 16 B; moving sphere 36 B;
+//   node fetch: the bytes loaded per visit (BVH2 64 B, BVH4 112 B, BVH8 224 B, compressed
+//   BVH8 96 B); sphere 16 B; moving sphere 36 B;
 //   rect 24 B; instance chain entered 32 B; medium record 16 B; material +
 //   texture per shade 16 + 16 B; Perlin turbulence 7 octaves x 8 gradient gathers
 //   x (12 B gradient + 3 x 4 B permutation) = 1344 B; per work item the 4-B job
@@ -128,7 +129,8 @@ rt_dprim to_dprim(const rt_prim &p, int order) {
 //   partial sums read back, the output index and the 12-B pixel — is not the
 //   megakernel's.)
 double algorithmic_bytes(const rt_stats &st, double items, int bvh_width) {
-    return (bvh_width == 4 ? 112.0 : 64.0) * st.node_visits + 16.0 * st.sphere_tests + 36.0 * st.moving_sphere_tests + 24.0 * st.rect_tests +
+    const double node = bvh_width == 4 ? 112.0 : bvh_width == 8 ? 224.0 : bvh_width == RT_BVH_CW8 ? 96.0 : 64.0;
+    return node * st.node_visits + 16.0 * st.sphere_tests + 36.0 * st.moving_sphere_tests + 24.0 * st.rect_tests +
            32.0 * st.instanced_tests + 16.0 * st.medium_tests + 32.0 * st.shades + 1344.0 * st.noise_evals +
            20.0 * items;
 }
@@ -364,8 +366,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             if (ref != RT_EMPTY_CHILD && (ref & RT_LEAF_BIT))
                 ref = RT_LEAF_REF(RT_LEAF_FIRST(ref) + K, RT_LEAF_COUNT(ref));
         };
-        for (auto &n : bvh.nodes2) for (int c = 0; c < 2; c++) shift(n.ch[c]);
-        for (auto &n : bvh.nodes4) for (int c = 0; c < 4; c++) shift(n.ch[c]);
+        bvh.for_each_ref(shift);
         shift(bvh.root);
         bvh.order.insert(bvh.order.begin(), big.begin(), big.end());
     }
@@ -496,6 +497,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
 
     Arena arena;
     if (bvh.width == 4) stage(arena, &s->nodes, bvh.nodes4);
+    else if (bvh.width == 8) stage(arena, &s->nodes, bvh.nodes8);
+    else if (bvh.width == RT_BVH_CW8) stage(arena, &s->nodes, bvh.nodes8q);
     else stage(arena, &s->nodes, bvh.nodes2);
     stage(arena, &s->prims, prims);
     stage(arena, &s->bprims, bprims);
@@ -514,7 +517,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->has_bvh = d->nprims > 0;
     s->nmedia = d->nmedia;
     s->bvh_depth = bvh.depth;
-    s->nnodes = (int)(bvh.width == 4 ? bvh.nodes4.size() : bvh.nodes2.size());
+    s->nnodes = (int)bvh.node_count();
     s->bvh_width = bvh.width;
     s->nprims = d->nprims;
     s->ninstances = d->ninstances;
@@ -686,6 +689,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.stack_depth = s->stack_depth;
     a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
                  (s->has_checker ? RT_FEAT_CHECKER : 0) | (s->nprescan > 0 ? RT_FEAT_PRESCAN : 0);
+    // RTNW_FEAT_ALL=1 runs the all-feature variant (the one the wide BVHs use): A/B runs only
+    if (const char *e = std::getenv("RTNW_FEAT_ALL")) if (std::atoi(e)) a.features = RT_FEAT_ALL;
     for (int k = 0; k < 3; k++) {
         a.org[k] = cam->origin[k];
         a.llc[k] = cam->lower_left_corner[k];
@@ -794,7 +799,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         stats->lds_level = s->lds_nodes ? 1.0 : 0.0;
         stats->scan_groups = s->scan ? (double)s->ngroups : 0.0;
         stats->prescan = (double)s->nprescan;
-        stats->stack_depth = (double)(s->lds_nodes ? s->stack_depth : RT_STACK_DEPTH);
+        stats->stack_depth = (double)(s->lds_nodes ? s->stack_depth : s->bvh_width >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH);
     }
     return RT_OK;
 }

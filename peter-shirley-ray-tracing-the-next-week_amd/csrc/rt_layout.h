@@ -12,6 +12,7 @@
 #include "rt_hip.h"   // enum values (prim / material / texture kinds, ops)
 
 #define RT_STACK_DEPTH 24          // traversal stack entries per lane (LDS)
+#define RT_STACK_DEPTH_W8 32       // the same for the 8-wide BVHs (up to 7 pushes per node)
 #define RT_MAX_BVH_DEPTH 23        // builder guarantee: a root-to-leaf path has <= 23 internal nodes
                                    // (a median split of 2^24 - 1 primitives, the ABI maximum, fits)
 #define RT_MAX_LEAF 8              // primitives per leaf
@@ -25,8 +26,8 @@
 #define RT_LEAF_FIRST(ref) ((ref) & 0x00FFFFFFu)
 #define RT_LEAF_COUNT(ref) ((((ref) >> 24) & 0x7Fu) + 1)
 
-// The BVH comes in two widths (RTNW_BVH_WIDTH, default 2), nodes numbered
-// breadth-first so the top levels are a prefix of the array (kept in LDS).
+// The BVH comes in four node forms (RTNW_BVH_WIDTH = 2 (default), 4, 8, 8q), nodes
+// numbered breadth-first so the top levels are a prefix of the array (kept in LDS).
 //
 // BVH2 node, 64 B: the boxes of BOTH children, so one node fetch decides which
 // children to enter:
@@ -47,12 +48,38 @@ struct rt_dnode2 {
 //   q[4] = z of c0, c1   q[5] = z of c2, c3      each (lo, hi, lo, hi)
 //   ch   = child references (RT_EMPTY_CHILD: unused slot)
 //   pad  = keeps nodes on 128-B lines; never read
-// Builder guarantee (both widths): along any root-to-leaf path the children
-// beyond the first sum to <= RT_STACK_DEPTH - 1, which bounds the traversal stack.
+// Builder guarantee (every width): along any root-to-leaf path the children
+// beyond the first sum to <= RT_STACK_DEPTH - 1 (8-wide: RT_STACK_DEPTH_W8 - 1),
+// which bounds the traversal stack.
 struct rt_dnode4 {
     float q[6][4];
     uint32_t ch[4];
     uint32_t pad[4];
+};
+
+// BVH8 node (RTNW_BVH_WIDTH=8), 256 B: as BVH4 with four pairs per axis,
+//   q[4a + p] = axis a of children 2p, 2p+1, (lo, hi, lo, hi);  ch = 8 references.
+struct rt_dnode8 {
+    float q[12][4];
+    uint32_t ch[8];
+    uint32_t pad[8];
+};
+
+// Compressed BVH8 node (RTNW_BVH_WIDTH=8q), 128 B: child boxes quantised to 8 bits
+// per plane on a per-axis power-of-two grid anchored at the node's box (Ylitie et
+// al., "Efficient incoherent ray traversal on GPUs through compressed wide BVHs",
+// HPG 2017).  Plane k of child c on axis a lies at origin[a] + q * 2^(e[a] - 127),
+// quantised outward (lo floored, hi ceiled), so the decoded box contains the child.
+//   origin, ebits = e_x | e_y << 8 | e_z << 16
+//   qa[a] = axis a: bytes of lo c0..c3, lo c4..c7, hi c0..c3, hi c4..c7
+//   ch = 8 references;  pad keeps 128-B lines
+#define RT_BVH_CW8 9               // RtKernelArgs.bvh_width of the compressed 8-wide layout
+struct rt_dnode8q {
+    float origin[3];
+    uint32_t ebits;
+    uint32_t qa[3][4];
+    uint32_t ch[8];
+    uint32_t pad[8];
 };
 
 // Primitive, 64 B, ordered so the first 32 B (g0, m) are all a sphere or rect test

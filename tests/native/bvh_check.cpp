@@ -1,5 +1,6 @@
 // tests/native/bvh_check.cpp — invariants of the BVH builder (csrc/host/bvh.cpp) that
-// the device traversal relies on, for both node widths, on the built-in scenes and
+// the device traversal relies on, for every node width (2, 4, 8 and the compressed
+// 8-wide form, whose boxes are decoded here as the device decodes them), on the built-in scenes and
 // on adversarial synthetic ones (run by tests/test_host_api.py):
 //   * every primitive is referenced by exactly one leaf, leaves hold <= RT_MAX_LEAF;
 //   * every child box contains its subtree's primitive boxes (non-instanced prims);
@@ -66,29 +67,48 @@ struct Checker {
         if (ref <= parent) err = "child numbered before its parent";
         node(width, ref, lo, hi);
     }
+    static int slots(int width) { return width == RT_BVH_CW8 ? 8 : width; }
+    // child c of node id: its reference and its box as the device reads it
+    uint32_t child_box(int width, uint32_t id, int c, float lo[3], float hi[3]) const {
+        if (width == 2) {
+            const rt_dnode2 &d = r.nodes2[id];
+            const float *f = &d.b[0][0] + 6 * c;
+            for (int a = 0; a < 3; a++) { lo[a] = f[2 * a]; hi[a] = f[2 * a + 1]; }
+            return d.ch[c];
+        }
+        if (width == 4 || width == 8) {
+            const float(*q)[4] = width == 4 ? r.nodes4[id].q : r.nodes8[id].q;
+            const int per_axis = width / 2;
+            for (int a = 0; a < 3; a++) {
+                const float *p = q[per_axis * a + (c >> 1)] + 2 * (c & 1);
+                lo[a] = p[0]; hi[a] = p[1];
+            }
+            return width == 4 ? r.nodes4[id].ch[c] : r.nodes8[id].ch[c];
+        }
+        const rt_dnode8q &d = r.nodes8q[id];
+        for (int a = 0; a < 3; a++) {
+            const double step = std::ldexp(1.0, (int)((d.ebits >> (8 * a)) & 0xFFu) - 127);
+            const uint32_t wl = d.qa[a][c >> 2], wh = d.qa[a][2 + (c >> 2)];
+            const double l = d.origin[a] + ((wl >> (8 * (c & 3))) & 0xFFu) * step;   // exact in double
+            const double h = d.origin[a] + ((wh >> (8 * (c & 3))) & 0xFFu) * step;
+            lo[a] = (float)l;
+            hi[a] = (float)h;
+            if ((double)lo[a] > l) lo[a] = std::nextafter(lo[a], -INFINITY);   // outward to float
+            if ((double)hi[a] < h) hi[a] = std::nextafter(hi[a], INFINITY);
+        }
+        return d.ch[c];
+    }
     // returns the stack bound of the subtree
     int node(int width, uint32_t id, const float plo[3], const float phi[3]) {
         int nch = 0, worst = 0;
-        for (int c = 0; c < width; c++) {
+        for (int c = 0; c < slots(width); c++) {
             float lo[3], hi[3];
-            uint32_t ref;
-            if (width == 2) {
-                const rt_dnode2 &d = r.nodes2[id];
-                const float *f = &d.b[0][0] + 6 * c;
-                for (int a = 0; a < 3; a++) { lo[a] = f[2 * a]; hi[a] = f[2 * a + 1]; }
-                ref = d.ch[c];
-            } else {
-                const rt_dnode4 &d = r.nodes4[id];
-                for (int a = 0; a < 3; a++) {
-                    const float *q = d.q[2 * a + (c >> 1)] + 2 * (c & 1);
-                    lo[a] = q[0]; hi[a] = q[1];
-                }
-                ref = d.ch[c];
-            }
+            const uint32_t ref = child_box(width, id, c, lo, hi);
             if (ref == RT_EMPTY_CHILD) continue;
             nch++;
+            // (a quantised box may reach up to one grid step past its parent's)
             for (int a = 0; a < 3; a++)
-                if (plo && (lo[a] < plo[a] || hi[a] > phi[a])) err = "child box outside its parent's box";
+                if (plo && width != RT_BVH_CW8 && (lo[a] < plo[a] || hi[a] > phi[a])) err = "child box outside its parent's box";
             if (!(ref & RT_LEAF_BIT)) worst = std::max(worst, bound_of(width, ref));
             child(width, ref, lo, hi, id);
         }
@@ -96,8 +116,9 @@ struct Checker {
     }
     int bound_of(int width, uint32_t id) {
         int nch = 0, worst = 0;
-        for (int c = 0; c < width; c++) {
-            const uint32_t ref = width == 2 ? r.nodes2[id].ch[c] : r.nodes4[id].ch[c];
+        for (int c = 0; c < slots(width); c++) {
+            float lo[3], hi[3];
+            const uint32_t ref = child_box(width, id, c, lo, hi);
             if (ref == RT_EMPTY_CHILD) continue;
             nch++;
             if (!(ref & RT_LEAF_BIT)) worst = std::max(worst, bound_of(width, ref));
@@ -108,26 +129,28 @@ struct Checker {
 
 int check(const char *name, const rt_prim *prims, int n, const rt_instance *inst, float t0, float t1) {
     int bad = 0;
-    for (int width : {2, 4}) {
-        setenv("RTNW_BVH_WIDTH", width == 4 ? "4" : "2", 1);
+    for (int width : {2, 4, 8, RT_BVH_CW8}) {
+        setenv("RTNW_BVH_WIDTH", width == RT_BVH_CW8 ? "8q" : std::to_string(width).c_str(), 1);
         const rtnw::BvhResult r = rtnw::build_bvh(prims, n, inst, t0, t1);
+        if (r.width != width) { std::printf("%s: built width %d, asked %d\n", name, r.width, width); return bad + 1; }
         Checker c{prims, n, r, std::vector<int>(n, 0), ""};
         int bound = 0;
         if (n == 0) {   // no primitives: no tree (the scene renders with has_bvh = 0)
-            if (!r.nodes2.empty() || !r.nodes4.empty() || !r.order.empty()) c.err = "a tree for an empty scene";
+            if (r.node_count() != 0 || !r.order.empty()) c.err = "a tree for an empty scene";
         } else if (r.root & RT_LEAF_BIT) {   // a single-leaf scene: the leaf is the root
             const float lo[3] = {-INFINITY, -INFINITY, -INFINITY}, hi[3] = {INFINITY, INFINITY, INFINITY};
             c.child(width, r.root, lo, hi, 0);
-            if (!(width == 2 ? r.nodes2.empty() : r.nodes4.empty())) c.err = "nodes emitted for a single-leaf scene";
+            if (r.node_count() != 0) c.err = "nodes emitted for a single-leaf scene";
         } else {
             c.node(width, r.root, nullptr, nullptr);
             bound = c.bound_of(width, r.root);
         }
         for (int i = 0; i < n && c.err.empty(); i++)
             if (c.seen[i] != 1) c.err = "primitive referenced " + std::to_string(c.seen[i]) + " times";
-        if (bound > RT_STACK_DEPTH - 1) c.err = "stack bound " + std::to_string(bound) + " exceeds the LDS stack";
+        const int cap = (width >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH) - 1;
+        if (bound > cap) c.err = "stack bound " + std::to_string(bound) + " exceeds the LDS stack";
         std::printf("%-16s width %d prims %7d nodes %6zu depth %2d stack-bound %2d %s\n", name, width, n,
-                    width == 2 ? r.nodes2.size() : r.nodes4.size(), r.depth, bound, c.err.empty() ? "ok" : c.err.c_str());
+                    r.node_count(), r.depth, bound, c.err.empty() ? "ok" : c.err.c_str());
         bad += !c.err.empty();
     }
     return bad;

@@ -367,7 +367,8 @@ def test_ppm_from_gpu_mean_matches_oracle_quantiser():
                                             ("edge_degenerate", 40, 20, 8)])
 def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     """The closest hit is fixed by (t, list order) whatever structure finds it: the
-    BVH's width (RTNW_BVH_WIDTH=2 or 4 at scene creation), where its nodes are read
+    BVH's node form (RTNW_BVH_WIDTH = 2, 4, 8 or 8q (compressed 8-wide) at scene
+    creation), where its nodes are read
     from (RTNW_LDS_BVH=1: the BVH2 copied to LDS, one 16-wave workgroup per CU; 0:
     HBM, 4-wave workgroups), or no BVH at all (the flat scan of instance groups that
     scenes of <= 64 primitives take unless RTNW_SCAN=0): the images must agree bit
@@ -377,7 +378,8 @@ def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, chunk=4, seed=11)
     out, how = {}, {}
     big = scene == "random_motion"   # its ground sphere spans the scene: pre-scanned (final(): none reach 10 %)
-    for width, lds, scan in (("2", "1", "1"), ("2", "1", "0"), ("2", "0", "0"), ("4", "1", "1")):
+    for width, lds, scan in (("2", "1", "1"), ("2", "1", "0"), ("2", "0", "0"), ("4", "1", "1"), ("8", "1", "1"),
+                             ("8q", "1", "1")):
         monkeypatch.setenv("RTNW_BVH_WIDTH", width)
         monkeypatch.setenv("RTNW_LDS_BVH", lds)
         monkeypatch.setenv("RTNW_SCAN", scan)
@@ -395,7 +397,7 @@ def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     nonempty = scene != "edge_empty"
     assert how == {("2", "1", "1"): (0.0, nonempty) if small else (1.0, False),
                    ("2", "1", "0"): (float(has_nodes), False), ("2", "0", "0"): (0.0, False),
-                   ("4", "1", "1"): (0.0, False)}, how
+                   ("4", "1", "1"): (0.0, False), ("8", "1", "1"): (0.0, False), ("8q", "1", "1"): (0.0, False)}, how
     ref = out["2", "0", "0"].view(np.uint32)
     for k, img in out.items():
         assert np.array_equal(img.view(np.uint32), ref), k

@@ -161,7 +161,7 @@ def test_device_log_matches_glibc(tmp_path):
 
 
 def test_bvh_builder_invariants(tmp_path):
-    """tests/native/bvh_check.cpp: for BVH widths 2 and 4, on every built-in scene and on
+    """tests/native/bvh_check.cpp: for BVH widths 2, 4, 8 and compressed 8, on every built-in scene and on
     adversarial synthetic ones (200k uniform, 50k identical, 20k geometric spheres):
     each primitive in exactly one leaf, child boxes contain their primitives,
     breadth-first numbering, and the stack bound within the 24-entry LDS stack."""

@@ -1,0 +1,126 @@
+// tools/microbench/valu_rates.hip — issue cost of the integer / f64 VALU instructions the
+// megakernel's RNG and media code use, on gfx950: 8 independent chains per wave, 8 waves
+// per SIMD on every CU, cycles per wave-instruction per SIMD from the kernel time.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define N_ITER 4096
+#define BODY8(S) S(x0) S(x1) S(x2) S(x3) S(x4) S(x5) S(x6) S(x7)
+
+#define K32(name, asmtxt)                                                                   \
+    __global__ __launch_bounds__(256) void name(uint32_t *out, uint32_t c) {                \
+        uint32_t x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,      \
+                 x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;                                     \
+        for (int i = 0; i < N_ITER; ++i) {                                                  \
+            _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                 \
+                BODY8(STEP)                                                                 \
+            }                                                                               \
+        }                                                                                   \
+        out[blockIdx.x * 256 + threadIdx.x] = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;        \
+    }
+#define STEP(x) asm volatile(ASM : "+v"(x) : "v"(c));
+#define ASM "v_add_u32 %0, %0, %1"
+K32(k_add_u32, ASM)
+#undef ASM
+#define ASM "v_mul_lo_u32 %0, %0, %1"
+K32(k_mul_lo_u32, ASM)
+#undef ASM
+#define ASM "v_mul_hi_u32 %0, %0, %1"
+K32(k_mul_hi_u32, ASM)
+#undef ASM
+#define ASM "v_mul_u32_u24 %0, %0, %1"
+K32(k_mul_u32_u24, ASM)
+#undef ASM
+#define ASM "v_mul_hi_u32_u24 %0, %0, %1"
+K32(k_mul_hi_u32_u24, ASM)
+#undef ASM
+#define ASM "v_xor_b32 %0, %0, %1"
+K32(k_xor_b32, ASM)
+#undef ASM
+#define ASM "v_alignbit_b32 %0, %0, %1, 13"
+K32(k_alignbit, ASM)
+#undef ASM
+#define ASM "v_fma_f32 %0, %0, %1, %1"
+K32(k_fma_f32, ASM)
+#undef ASM
+#undef STEP
+
+#define K64(name, asmtxt)                                                                   \
+    __global__ __launch_bounds__(256) void name(uint32_t *out, uint32_t c) {                \
+        uint64_t x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,      \
+                 x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;                                     \
+        uint64_t cc = c;                                                                    \
+        for (int i = 0; i < N_ITER; ++i) {                                                  \
+            _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                 \
+                BODY8(STEP)                                                                 \
+            }                                                                               \
+        }                                                                                   \
+        out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)(x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7); \
+    }
+#define STEP(x) asm volatile(ASM : "+v"(x) : "v"(cc));
+#define ASM "v_mad_u64_u32 %0, vcc, %0, %1, %0"
+#undef ASM
+#define ASM "v_lshrrev_b64 %0, 27, %0"
+K64(k_lshr_b64, ASM)
+#undef ASM
+#define ASM "v_add_f64 %0, %0, %1"
+K64(k_add_f64, ASM)
+#undef ASM
+#define ASM "v_fma_f64 %0, %0, %1, %1"
+K64(k_fma_f64, ASM)
+#undef ASM
+#define ASM "v_lshl_add_u64 %0, %0, 0, %1"
+K64(k_lshl_add_u64, ASM)
+#undef ASM
+#undef STEP
+
+// v_mad_u64_u32 writes a 64-bit result from two 32-bit sources
+__global__ __launch_bounds__(256) void k_mad_u64_u32(uint32_t *out, uint32_t c) {
+    uint64_t x[8];
+    for (int j = 0; j < 8; ++j) x[j] = threadIdx.x + j;
+    for (int i = 0; i < N_ITER; ++i) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                uint32_t lo = (uint32_t)x[j];
+                asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(x[j]) : "v"(lo), "v"(c) : "vcc");
+            }
+        }
+    }
+    uint64_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= x[j];
+    out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)r;
+}
+
+int main() {
+    int dev = 0, cus = 0, clk = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, dev);   // kHz
+    const int waves_per_simd = 8, blocks = cus * waves_per_simd;      // 4 waves per block -> 1 per SIMD
+    uint32_t *out;
+    hipMalloc(&out, (size_t)blocks * 256 * 4);
+    struct { const char *name; void (*k)(uint32_t *, uint32_t); } ks[] = {
+        {"v_add_u32", k_add_u32}, {"v_xor_b32", k_xor_b32}, {"v_fma_f32", k_fma_f32},
+        {"v_alignbit_b32", k_alignbit}, {"v_mul_u32_u24", k_mul_u32_u24}, {"v_mul_hi_u32_u24", k_mul_hi_u32_u24},
+        {"v_mul_lo_u32", k_mul_lo_u32}, {"v_mul_hi_u32", k_mul_hi_u32}, {"v_mad_u64_u32", k_mad_u64_u32},
+        {"v_lshrrev_b64", k_lshr_b64}, {"v_lshl_add_u64", k_lshl_add_u64}, {"v_add_f64", k_add_f64},
+        {"v_fma_f64", k_fma_f64}};
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    for (auto &k : ks) {
+        hipLaunchKernelGGL(k.k, dim3(blocks), dim3(256), 0, 0, out, 0x9E3779B9u);
+        hipEventRecord(a);
+        hipLaunchKernelGGL(k.k, dim3(blocks), dim3(256), 0, 0, out, 0x9E3779B9u);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        const double insts_per_simd = (double)waves_per_simd * N_ITER * 32;
+        const double cyc = ms * 1e-3 * clk * 1e3 / insts_per_simd;
+        printf("%-18s %8.3f ms  %6.2f cycles per wave-instruction per SIMD (clock %d MHz)\n", k.name, ms, cyc, clk / 1000);
+    }
+    return 0;
+}

@@ -22,8 +22,8 @@ for line in err.splitlines():
     if m and cur:
         rows[cur][m.group(1).strip()] = int(m.group(2))
 for name, r in rows.items():
-    m = re.search(r"rt_megakernelILb(\d)ELb(\d)ELi(\d)ELi(\d)E", name)
-    tag = f"mega count={m.group(1)} prof={m.group(2)} width={m.group(3)} feat={m.group(4)}" if m else name[:40]
+    m = re.search(r"rt_megakernelILb(\d)ELb(\d)ELi(\d+)ELi(\d+)ELi(\d)E", name)
+    tag = f"mega count={m.group(1)} prof={m.group(2)} width={m.group(3)} feat={m.group(4)} mode={m.group(5)}" if m else name[:40]
     print(f"{tag:44s} VGPR {r.get('VGPRs')} AGPR {r.get('AGPRs')} SGPR {r.get('TotalSGPRs')} "
           f"scratch {r.get('ScratchSize [bytes/lane]')} waves {r.get('Occupancy [waves/SIMD]')} "
           f"LDS {r.get('LDS Size [bytes/block]')}")
