@@ -554,10 +554,10 @@ struct GlobalNodes {
     __device__ __forceinline__ const float4 *ptr8(uint32_t n) const { return p + n * 16; }
     __device__ __forceinline__ const float4 *ptr8q(uint32_t n) const { return p + n * 8; }
 };
-struct LdsNodes {
+struct LdsNodes {   // node references are byte offsets (n * 16) into the planes
     const LdsF4 *p;
     __device__ __forceinline__ void load2(uint32_t n, float4 &b0, float4 &b1, float4 &b2, float4 &cf) const {
-        const LdsF4 *N = p + n;
+        const LdsF4 *N = (const LdsF4 *)((__attribute__((address_space(3))) const char *)p + n);
         b0 = f4(N[0]); b1 = f4(N[RT_LDS_NODE_CAP]); b2 = f4(N[2 * RT_LDS_NODE_CAP]); cf = f4(N[3 * RT_LDS_NODE_CAP]);
     }
     __device__ __forceinline__ const float4 *ptr4(uint32_t) const { return nullptr; }   // wide BVHs stay in HBM
@@ -722,7 +722,7 @@ __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, 
             node = park ? RT_EMPTY_CHILD : node;
             const bool pop = node == RT_EMPTY_CHILD && sp > 0;
             sp -= pop ? 1 : 0;
-            const uint32_t top = stk[(sp > 0 ? sp : 0) * 64];
+            const uint32_t top = stk[(uint32_t)sp * 64u];   // sp >= 0: pops only from a non-empty stack
             node = pop ? top : node;
         }
         if (__popcll(wballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD)) <= kTail) return pleaf;

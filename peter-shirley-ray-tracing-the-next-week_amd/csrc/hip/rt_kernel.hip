@@ -88,9 +88,15 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) store_camera(A, lds_cam);
     if (kLds) {
+        // interior child references become byte offsets into the planes (n * 16): a
+        // node step's LDS address is then the reference itself (LdsNodes)
         for (uint32_t i = threadIdx.x; i < A.nnodes; i += kBlock) {
             const float4 *N = A.nodes + i * 4;
-            const float4 b0 = N[0], b1 = N[1], b2 = N[2], cf = N[3];
+            const float4 b0 = N[0], b1 = N[1], b2 = N[2];
+            float4 cf = N[3];
+            const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
+            cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : c0 << 4);
+            cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : c1 << 4);
             lds_dyn[i] = b0;
             lds_dyn[i + RT_LDS_NODE_CAP] = b1;
             lds_dyn[i + 2 * RT_LDS_NODE_CAP] = b2;
@@ -144,7 +150,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     bool fresh = false;   // a new segment the pre-scan has not seen yet
     auto begin_segment = [&]() {
         if (kPrescan) fresh = true;
-        node = A.root;
+        node = kLds ? A.root << 4 : A.root;   // LDS mode: byte offsets (the root is interior there)
         sp = 0;
         best_t = RT_FLT_MAX;
         best_key = 0x7FFFFFFF;
