@@ -22,12 +22,17 @@ Workloads (BASELINE.json configs):
   --config c2 / c3 / c4 with N > 1: weak scaling, N x the 1-GPU pixels.
 
 Prints ONE JSON line (rank 0) with
-  roofline: the megakernel is bound by VALU instruction issue: the
-    wave-level VALU instructions of one launch (SQ_INSTS_VALU per sample from the
-    committed rocprofv3 pass, profiles/r<NN>/traffic.json, for this very library
-    build) over the kernel's live HIP-event time, against 1,024 SIMDs x 2.4 GHz / 2
-    cycles per wave64 VALU instruction; hbm_frac = PMC-measured HBM bytes per launch
-    over the same time vs 8 TB/s; cache_served_bytes = SURVEY §8d's byte model.
+  roofline: the megakernel is bound by VALU instruction issue.
+    achieved = the wave-level VALU instructions of one launch (SQ_INSTS_VALU per
+    sample from the committed rocprofv3 pass, profiles/r<NN>/traffic.json, for this
+    very library build) over the kernel's live HIP-event time; peak = the rate 1,024
+    SIMDs x 2.4 GHz sustain on THIS kernel's instruction mix: each PMC instruction
+    class charged its microbenchmarked issue cost (tools/valu_issue_model.py:
+    ~2.4 cycles for f32 add/mul, integer add, logic and moves, ~4.2 for FMA,
+    min/max, compares, selects, shifts and 64-bit ops, ~8.2 for transcendentals).
+    frac_uniform_2cyc keeps round 1's optimistic roof (every instruction 2 cycles).
+    hbm_frac = PMC-measured HBM bytes per launch over the same time vs 8 TB/s;
+    cache_served_bytes = SURVEY §8d's byte model.
   cpu_baseline: the reference binary (oracle/_ref/ref_render, compiled from the
     reference's own sources) on this job's CPU cores, bounded sample; the flat list
     as shipped (main.cpp:291) and with a corrected BVH (bvh.h:29-54, slab fixed).
@@ -321,8 +326,9 @@ def main():
     cache_bytes = cst["algorithmic_bytes"]
     sha = lib_sha16()
     prof = read_profile("c4" if cfg in ("c4", "c5") and scene_name == "final" else cfg, sha)
-    roof = {"bound": "valu_issue", "achieved": None, "peak": VALU_PEAK / 1e9, "unit": "G wave-VALU-instr/s",
+    roof = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G wave-VALU-instr/s",
             "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
+            "frac_uniform_2cyc": None, "valu_issue_cycles_per_instr": None,
             "lds_level": int(st["lds_level"]), "stack_depth": int(st["stack_depth"]), "scan_groups": int(st["scan_groups"]), "prescan": int(st["prescan"]),
             "batches_per_step": int(st["batches"]),
             "valu_insts_per_sample": None, "profile": None, "profile_matches_library": None,
@@ -335,9 +341,12 @@ def main():
             / max(1.0, cst["segments"]),
             "note": "the scene is L2/L1-resident: HBM carries ~1% of peak, the kernel is VALU-issue bound "
                     "(DESIGN.md §5c).  achieved = SQ_INSTS_VALU per sample (committed rocprofv3 pass of this "
-                    "library build) x samples / live kernel time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles; "
-                    "traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE); cache_served = SURVEY "
-                    "§8d byte model (node/primitive fetches, mostly L1/L2 hits)"}
+                    "library build) x samples / live kernel time; peak = 1024 SIMDs x 2.4 GHz / the mean "
+                    "issue cycles per instruction of this kernel's mix (PMC instruction classes x "
+                    "microbenchmarked costs, tools/valu_issue_model.py); frac_uniform_2cyc = the same "
+                    "instructions against 2 cycles each; traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 "
+                    "+ WRITE_SIZE); cache_served = SURVEY §8d byte model (node/primitive fetches, mostly "
+                    "L1/L2 hits)"}
     if prof:
         roof["profile"] = prof["path"]
         roof["profile_matches_library"] = prof.get("lib_sha16") == sha
@@ -345,7 +354,13 @@ def main():
             vi = prof["valu_insts_per_sample"] * rank_samples
             roof["valu_insts_per_sample"] = prof["valu_insts_per_sample"]
             roof["achieved"] = vi / avg_kernel_s / 1e9
-            roof["frac"] = vi / avg_kernel_s / VALU_PEAK
+            roof["frac_uniform_2cyc"] = vi / avg_kernel_s / VALU_PEAK
+            cpi = prof.get("valu_issue_cycles_per_instr")
+            if cpi:
+                peak = SIMDS * CLOCK_GHZ * 1e9 / cpi
+                roof["valu_issue_cycles_per_instr"] = cpi
+                roof["peak"] = peak / 1e9
+                roof["frac"] = vi / avg_kernel_s / peak
         if prof.get("hbm_bytes_per_sample"):
             tr = prof["hbm_bytes_per_sample"] * rank_samples
             roof["traffic"] = tr

@@ -1,14 +1,17 @@
 #!/bin/bash
 # tools/final_profile.sh — the round's evidence for the library in the tree, on the
-# gpurun box: PMC passes of the timed c4 megakernel (separate rocprofv3 passes) and
-# their summary (traffic.json, read by bench.py's roofline), a kernel-trace --stats
-# run of bench.py, and the bench lines of c4 (with the CPU baseline), c2, c3, c5.
-# Every step under its own time limit; the first failure ends the script.
+# gpurun box: PMC passes of the timed c4 megakernel (separate rocprofv3 passes: HBM
+# bytes, L2, SQ occupancy/waits, and the two VALU instruction-class passes), the
+# per-instruction issue-cost microbenchmark.  Every step under its own time limit;
+# the first failure ends the script.  Then, on the build host, the summary
+# (traffic.json with the issue-weighted VALU model, which bench.py's roofline reads):
+#   python3 tools/pmc_traffic.py gpurun_out/final profiles/r<NN> 250000000 c4
+# and back on the box tools/final_bench.sh (kernel trace + bench lines).
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/final
-mkdir -p $O
+mkdir -p $O/classes
 B="python3 bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline"
 for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:l2" \
             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE:sq"; do
@@ -16,14 +19,13 @@ for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:l2" 
   echo "== pmc $name"
   timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/pmc_$name -o run --output-format csv -- $B > $O/pmc_$name.log 2>&1
 done
-python3 tools/pmc_traffic.py $O $O/summary 250000000 c4
-echo "== kernel trace"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
-    python3 bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline > $O/prof.log 2>&1
-echo "== bench c4"
-timeout -k 10 400 python3 bench.py > $O/bench_c4.log 2>&1
-for c in c2 c3 c5; do
-  echo "== bench $c"
-  timeout -k 10 300 python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_$c.log 2>&1
+i=0
+for ctrs in "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT" \
+            "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH"; do
+  i=$((i+1))
+  echo "== pmc classes $i"
+  timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/classes/c4_$i -o run --output-format csv -- $B > $O/classes/c4_$i.log 2>&1
 done
+echo "== microbenchmark"
+timeout -k 10 120 tools/microbench/valu_rates > $O/valu_rates.log 2>&1
 echo done

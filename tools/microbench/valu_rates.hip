@@ -44,6 +44,77 @@ K32(k_alignbit, ASM)
 #define ASM "v_fma_f32 %0, %0, %1, %1"
 K32(k_fma_f32, ASM)
 #undef ASM
+#define ASM "v_add_f32 %0, %0, %1"
+K32(k_add_f32, ASM)
+#undef ASM
+#define ASM "v_mul_f32 %0, %0, %1"
+K32(k_mul_f32, ASM)
+#undef ASM
+#define ASM "v_max_f32 %0, %0, %1"
+K32(k_max_f32, ASM)
+#undef ASM
+#define ASM "v_min3_f32 %0, %0, %1, %0"
+K32(k_min3_f32, ASM)
+#undef ASM
+#define ASM "v_cndmask_b32 %0, %0, %1, vcc"
+K32(k_cndmask, ASM)
+#undef ASM
+#define ASM "v_mov_b32 %0, %1"
+K32(k_mov_b32, ASM)
+#undef ASM
+#define ASM "v_cmp_lt_f32 vcc, %0, %1"
+K32(k_cmp_f32, ASM)
+#undef ASM
+#define ASM "v_sqrt_f32 %0, %0"
+K32(k_sqrt_f32, ASM)
+#undef ASM
+#define ASM "v_rcp_f32 %0, %0"
+K32(k_rcp_f32, ASM)
+#undef ASM
+#define ASM "v_cvt_f32_ubyte1 %0, %0"
+K32(k_cvt_ubyte, ASM)
+#undef ASM
+#define ASM "v_fmac_f32 %0, %1, %1"
+K32(k_fmac_f32, ASM)
+#undef ASM
+#define ASM "v_sub_f32 %0, %0, %1"
+K32(k_sub_f32, ASM)
+#undef ASM
+#define ASM "v_min_f32 %0, %0, %1"
+K32(k_min_f32, ASM)
+#undef ASM
+#define ASM "v_max_i32 %0, %0, %1"
+K32(k_max_i32, ASM)
+#undef ASM
+#define ASM "v_med3_f32 %0, %0, %1, %1"
+K32(k_med3_f32, ASM)
+#undef ASM
+#define ASM "v_and_b32 %0, %0, %1"
+K32(k_and_b32, ASM)
+#undef ASM
+#define ASM "v_lshlrev_b32 %0, 3, %0"
+K32(k_lshl_b32, ASM)
+#undef ASM
+#define ASM "v_bfe_u32 %0, %0, 3, 7"
+K32(k_bfe_u32, ASM)
+#undef ASM
+#define ASM "v_cndmask_b32_e64 %0, %0, %1, s[40:41]"
+K32(k_cndmask_s, ASM)
+#undef ASM
+#define ASM "v_perm_b32 %0, %0, %1, %1"
+K32(k_perm_b32, ASM)
+#undef ASM
+#define ASM "v_max_f32_e64 %0, %0, %1"
+K32(k_max_f32_e64, ASM)
+#undef ASM
+#define ASM "v_mul_f32_e64 %0, %0, %1"
+K32(k_mul_f32_e64, ASM)
+#undef ASM
+#define ASM "v_add3_u32 %0, %0, %1, %1"
+K32(k_add3_u32, ASM)
+#undef ASM
+#define ASM "v_cvt_f32_f64 %0, %1"
+#undef ASM
 #undef STEP
 
 #define K64(name, asmtxt)                                                                   \
@@ -72,6 +143,18 @@ K64(k_fma_f64, ASM)
 #undef ASM
 #define ASM "v_lshl_add_u64 %0, %0, 0, %1"
 K64(k_lshl_add_u64, ASM)
+#undef ASM
+#define ASM "v_pk_fma_f32 %0, %0, %1, %1"
+K64(k_pk_fma_f32, ASM)
+#undef ASM
+#define ASM "v_pk_add_f32 %0, %0, %1"
+K64(k_pk_add_f32, ASM)
+#undef ASM
+#define ASM "v_pk_mul_f32 %0, %0, %1"
+K64(k_pk_mul_f32, ASM)
+#undef ASM
+#define ASM "v_mov_b64 %0, %1"
+K64(k_mov_b64, ASM)
 #undef ASM
 #undef STEP
 
@@ -106,7 +189,14 @@ int main() {
         {"v_alignbit_b32", k_alignbit}, {"v_mul_u32_u24", k_mul_u32_u24}, {"v_mul_hi_u32_u24", k_mul_hi_u32_u24},
         {"v_mul_lo_u32", k_mul_lo_u32}, {"v_mul_hi_u32", k_mul_hi_u32}, {"v_mad_u64_u32", k_mad_u64_u32},
         {"v_lshrrev_b64", k_lshr_b64}, {"v_lshl_add_u64", k_lshl_add_u64}, {"v_add_f64", k_add_f64},
-        {"v_fma_f64", k_fma_f64}};
+        {"v_fma_f64", k_fma_f64}, {"v_add_f32", k_add_f32}, {"v_mul_f32", k_mul_f32}, {"v_max_f32", k_max_f32},
+        {"v_min3_f32", k_min3_f32}, {"v_cndmask_b32", k_cndmask}, {"v_mov_b32", k_mov_b32}, {"v_cmp_lt_f32", k_cmp_f32},
+        {"v_sqrt_f32", k_sqrt_f32}, {"v_rcp_f32", k_rcp_f32}, {"v_cvt_f32_ubyte1", k_cvt_ubyte},
+        {"v_pk_fma_f32", k_pk_fma_f32}, {"v_pk_add_f32", k_pk_add_f32}, {"v_pk_mul_f32", k_pk_mul_f32},
+        {"v_mov_b64", k_mov_b64}, {"v_fmac_f32", k_fmac_f32}, {"v_sub_f32", k_sub_f32}, {"v_min_f32", k_min_f32},
+        {"v_max_i32", k_max_i32}, {"v_med3_f32", k_med3_f32}, {"v_and_b32", k_and_b32}, {"v_lshlrev_b32", k_lshl_b32},
+        {"v_bfe_u32", k_bfe_u32}, {"v_cndmask_b32 (sgpr mask)", k_cndmask_s}, {"v_perm_b32", k_perm_b32},
+        {"v_max_f32_e64", k_max_f32_e64}, {"v_mul_f32_e64", k_mul_f32_e64}, {"v_add3_u32", k_add3_u32}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);

@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
 """tools/pmc_traffic.py OUTDIR PROFILE_DIR [SAMPLES] [CONFIG] — summarises rocprofv3 PMC passes of bench.py.
 
+With OUTDIR/classes/ (tools/pmc_classes.sh) and the microbenchmark costs
+(profiles/r<NN>/valu_rates.log, env RT_VALU_RATES), it also adds the issue-weighted
+VALU model of tools/valu_issue_model.py (run on the build host: it compiles the
+kernel's assembly for the static opcode mix).
+
 Reads OUTDIR/pmc_{fetch,write,l2,sq}/run_counter_collection.csv (separate passes, as
 MI355X_MICROARCH.md §rocprofv3 requires: FETCH_SIZE and WRITE_SIZE do not fit one
 pass), keeps the dispatches of the timed megakernel (rt_megakernel<false, false>),
@@ -21,6 +26,7 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 KERNEL = os.environ.get("RT_PMC_KERNEL", "rt_megakernel<false, false")
 
 
@@ -79,6 +85,19 @@ def main():
         res["waves"] = sq["SQ_WAVES"]
         res["rocprof_VGPR_Count"] = sq["vgpr"]   # rocprof's field (the code object says 128 VGPRs)
         res["scratch_bytes_per_lane"] = sq["scratch"]
+    classes = os.path.join(out, "classes")
+    rates = os.environ.get("RT_VALU_RATES", os.path.join(prof, "valu_rates.log"))
+    if os.path.isdir(classes) and os.path.exists(rates):
+        import valu_issue_model as vim
+        model_path = os.path.join(prof, "valu_issue_model.json")
+        sys.argv = ["valu_issue_model.py", rates, classes, model_path, "", str(samples)]
+        vim.main()
+        with open(model_path) as f:
+            m = json.load(f)
+        res["valu_issue_cycles_per_sample"] = m["valu_issue_cycles_per_sample"]
+        res["valu_issue_cycles_per_instr"] = m["valu_issue_cycles_per_launch"] / m["valu_insts_per_launch"]
+        res["valu_issue_frac_weighted"] = m["valu_issue_frac_pmc_pass"]
+        res["valu_issue_model"] = os.path.relpath(model_path, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, "traffic.json"), "w") as f:
         json.dump(res, f, indent=1)
