@@ -325,7 +325,10 @@ def main():
     cst = scene.render_tiles(cam, cnt, tiles, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream, stats=True)
     cache_bytes = cst["algorithmic_bytes"]
     sha = lib_sha16()
-    prof = read_profile("c4" if cfg in ("c4", "c5") and scene_name == "final" else cfg, sha)
+    # the PMC profile of this config (c5 on several GPUs: c4's, whose per-sample wave
+    # coherence is the closer one — an interleaved rank's 8x8 work block spans 32x16
+    # pixels of the 1000^2 view, against 8x8 of c4's 500^2 and 8x8 of c5's on one GPU)
+    prof = read_profile(cfg, sha) or (read_profile("c4", sha) if cfg == "c5" and world > 1 else None)
     roof = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G wave-VALU-instr/s",
             "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
             "frac_uniform_2cyc": None, "valu_issue_cycles_per_instr": None,
@@ -357,7 +360,9 @@ def main():
             roof["frac_uniform_2cyc"] = vi / avg_kernel_s / VALU_PEAK
             cpi = prof.get("valu_issue_cycles_per_instr")
             if cpi:
-                peak = SIMDS * CLOCK_GHZ * 1e9 / cpi
+                clock = prof.get("effective_clock_ghz") or CLOCK_GHZ   # the kernel's clock in the PMC pass
+                peak = SIMDS * clock * 1e9 / cpi
+                roof["clock_ghz"] = clock
                 roof["valu_issue_cycles_per_instr"] = cpi
                 roof["peak"] = peak / 1e9
                 roof["frac"] = vi / avg_kernel_s / peak

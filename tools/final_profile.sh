@@ -5,14 +5,17 @@
 # per-instruction issue-cost microbenchmark.  Every step under its own time limit;
 # the first failure ends the script.  Then, on the build host, the summary
 # (traffic.json with the issue-weighted VALU model, which bench.py's roofline reads):
-#   python3 tools/pmc_traffic.py gpurun_out/final profiles/r<NN> 250000000 c4
+#   python3 tools/pmc_traffic.py gpurun_out/final_c4 profiles/r<NN> 250000000 c4
+# (c2 / c3 / c5: profiles/r<NN>/<cfg>, samples per launch 32e6 / 160e6 / 500e6 — c5
+# on one GPU runs as two sample batches)
 # and back on the box tools/final_bench.sh (kernel trace + bench lines).
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/final
+CFG=${1:-c4}   # the bench config profiled (c4 = the metric's; c2, c3, c5 for their own bench lines)
+O=gpurun_out/final_$CFG
 mkdir -p $O/classes
-B="python3 bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline"
+B="python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline"
 for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:l2" \
             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE:sq"; do
   ctrs=${pass%%:*}; name=${pass##*:}
@@ -24,8 +27,10 @@ for ctrs in "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_
             "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH"; do
   i=$((i+1))
   echo "== pmc classes $i"
-  timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/classes/c4_$i -o run --output-format csv -- $B > $O/classes/c4_$i.log 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/classes/pass$i -o run --output-format csv -- $B > $O/classes/pass$i.log 2>&1
 done
-echo "== microbenchmark"
-timeout -k 10 120 tools/microbench/valu_rates > $O/valu_rates.log 2>&1
+if [ "$CFG" = c4 ]; then
+  echo "== microbenchmark"
+  timeout -k 10 120 tools/microbench/valu_rates > $O/valu_rates.log 2>&1
+fi
 echo done

@@ -6,10 +6,20 @@
 #include <stdio.h>
 
 #define N_ITER 4096
+// shader clock of the run: block 0's first wave stamps s_memtime (shader cycles) and
+// s_memrealtime (100 MHz) at its start and end (MI355X_MICROARCH.md, in-kernel clock);
+// the stores are plain vector stores of lane 0
+__device__ unsigned long long g_stamps[4];
+#define STAMP(k)                                                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                              \
+        g_stamps[k] = __builtin_amdgcn_s_memtime();                                         \
+        g_stamps[k + 1] = __builtin_amdgcn_s_memrealtime();                                 \
+    }
 #define BODY8(S) S(x0) S(x1) S(x2) S(x3) S(x4) S(x5) S(x6) S(x7)
 
 #define K32(name, asmtxt)                                                                   \
     __global__ __launch_bounds__(256) void name(uint32_t *out, uint32_t c) {                \
+        STAMP(0)                                                                            \
         uint32_t x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,      \
                  x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;                                     \
         for (int i = 0; i < N_ITER; ++i) {                                                  \
@@ -18,6 +28,7 @@
             }                                                                               \
         }                                                                                   \
         out[blockIdx.x * 256 + threadIdx.x] = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;        \
+        STAMP(2)                                                                            \
     }
 #define STEP(x) asm volatile(ASM : "+v"(x) : "v"(c));
 #define ASM "v_add_u32 %0, %0, %1"
@@ -119,6 +130,7 @@ K32(k_add3_u32, ASM)
 
 #define K64(name, asmtxt)                                                                   \
     __global__ __launch_bounds__(256) void name(uint32_t *out, uint32_t c) {                \
+        STAMP(0)                                                                            \
         uint64_t x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,      \
                  x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;                                     \
         uint64_t cc = c;                                                                    \
@@ -128,6 +140,7 @@ K32(k_add3_u32, ASM)
             }                                                                               \
         }                                                                                   \
         out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)(x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7); \
+        STAMP(2)                                                                            \
     }
 #define STEP(x) asm volatile(ASM : "+v"(x) : "v"(cc));
 #define ASM "v_mad_u64_u32 %0, vcc, %0, %1, %0"
@@ -160,6 +173,7 @@ K64(k_mov_b64, ASM)
 
 // v_mad_u64_u32 writes a 64-bit result from two 32-bit sources
 __global__ __launch_bounds__(256) void k_mad_u64_u32(uint32_t *out, uint32_t c) {
+    STAMP(0)
     uint64_t x[8];
     for (int j = 0; j < 8; ++j) x[j] = threadIdx.x + j;
     for (int i = 0; i < N_ITER; ++i) {
@@ -175,6 +189,7 @@ __global__ __launch_bounds__(256) void k_mad_u64_u32(uint32_t *out, uint32_t c) 
     uint64_t r = 0;
     for (int j = 0; j < 8; ++j) r ^= x[j];
     out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)r;
+    STAMP(2)
 }
 
 int main() {
@@ -208,9 +223,13 @@ int main() {
         hipEventSynchronize(b);
         float ms = 0;
         hipEventElapsedTime(&ms, a, b);
+        unsigned long long st[4];
+        hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st);
+        const double mhz = (double)(st[2] - st[0]) / (double)(st[3] - st[1]) * 100.0;   // shader cycles per 10 ns
         const double insts_per_simd = (double)waves_per_simd * N_ITER * 32;
         const double cyc = ms * 1e-3 * clk * 1e3 / insts_per_simd;
-        printf("%-18s %8.3f ms  %6.2f cycles per wave-instruction per SIMD (clock %d MHz)\n", k.name, ms, cyc, clk / 1000);
+        printf("%-18s %8.3f ms  %6.2f cycles per wave-instruction per SIMD (clock %d MHz)  measured clock %.0f MHz: %.2f cycles\n",
+               k.name, ms, cyc, clk / 1000, mhz, ms * 1e-3 * mhz * 1e6 / insts_per_simd);
     }
     return 0;
 }

@@ -89,8 +89,10 @@ def main():
     rates = os.environ.get("RT_VALU_RATES", os.path.join(prof, "valu_rates.log"))
     if os.path.isdir(classes) and os.path.exists(rates):
         import valu_issue_model as vim
+        os.makedirs(prof, exist_ok=True)
         model_path = os.path.join(prof, "valu_issue_model.json")
-        sys.argv = ["valu_issue_model.py", rates, classes, model_path, "", str(samples)]
+        clock = str(res.get("effective_clock_ghz", ""))   # the SQ pass's GRBM clock
+        sys.argv = ["valu_issue_model.py", rates, classes, model_path, "", str(samples), config, clock]
         vim.main()
         with open(model_path) as f:
             m = json.load(f)

@@ -19,11 +19,12 @@ The model:
     each opcode appears in the kernel's code object (static mix within the class —
     the one assumption; the class totals themselves are measured);
   * demand = sum(class count x class cost) cycles, over 1024 SIMDs.
-frac = demand / (kernel time x 2.4 GHz): the share of the SIMDs' issue capacity
-the kernel's VALU instructions need.
+frac = demand / (kernel time x the kernel's own clock, GRBM_GUI_ACTIVE / 8 / time of
+the SQ pass): the share of the SIMDs' issue capacity the kernel's VALU instructions
+need.  Costs are in cycles at the clock each microbenchmark kernel measured for itself.
 
-usage: valu_issue_model.py RATES_LOG CLASSES_DIR OUT_JSON [ISA_S] [SAMPLES]
-  CLASSES_DIR holds c4_1/ and c4_2/ rocprofv3 outputs (tools/pmc_classes.sh);
+usage: valu_issue_model.py RATES_LOG CLASSES_DIR OUT_JSON [ISA_S] [SAMPLES] [CONFIG] [CLOCK_GHZ]
+  CLASSES_DIR holds pass1/ and pass2/ rocprofv3 outputs (tools/final_profile.sh);
   ISA_S = the device assembly (hipcc --cuda-device-only -S of rt_kernel.hip); built
   here when omitted.
 """
@@ -38,7 +39,14 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "peter-shirley-ray-tracing-the-next-week_amd")
-SYMBOL = "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi0ELi1EEEv12RtKernelArgs"   # c4: plain, BVH2, no features, LDS
+# the timed variant per config: <count, profile, width, features, mode>
+SYMBOLS = {
+    "c4": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi0ELi1EEEv12RtKernelArgs",    # final(): no features, LDS BVH2
+    "c5": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi0ELi1EEEv12RtKernelArgs",
+    "c3": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi12ELi1EEEv12RtKernelArgs",   # random_motion: checker + pre-scan
+    "c2": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi1ELi2EEEv12RtKernelArgs",    # cornell_box: instances, flat scan
+}
+SYMBOL = SYMBOLS["c4"]
 CLOCK_HZ = 2.4e9
 SIMDS = 1024
 
@@ -70,6 +78,10 @@ def measured_costs(path):
         if not m:
             continue
         name, sgpr, cyc = m.group(1), m.group(2), float(m.group(3))
+        # cycles at the clock the kernel measured itself (s_memtime / s_memrealtime), when sane
+        mc = re.search(r"measured clock (\d+) MHz: ([\d.]+) cycles", line)
+        if mc and 1500 <= int(mc.group(1)) <= 2600:
+            cyc = float(mc.group(2))
         if name == "v_cndmask_b32" and not sgpr:
             continue   # the VCC-mask form measured a hazard of the harness, not the issue cost
         costs[name] = cyc
@@ -90,11 +102,11 @@ def cost_of(op, costs):
     return costs.get("v_fma_f32", 4.2) if op.startswith("v_fma") else costs.get("v_min3_f32", 4.2)
 
 
-def static_opcodes(isa_path):
+def static_opcodes(isa_path, symbol):
     ops = collections.Counter()
     inside = False
     for line in open(isa_path):
-        if line.startswith(SYMBOL + ":"):
+        if line.startswith(symbol + ":"):
             inside = True
             continue
         if inside and "s_endpgm" in line:
@@ -116,8 +128,10 @@ def class_of(op):
 
 def pmc_counts(classes_dir):
     tot = {}
-    for sub in ("c4_1", "c4_2"):
+    for sub in ("pass1", "pass2"):   # rocprofv3 output dirs, or the copies committed under profiles/
         path = os.path.join(classes_dir, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            path = os.path.join(classes_dir, "pmc_classes_%s.csv" % sub[-1])
         for r in csv.DictReader(open(path)):
             if "rt_megakernel<false, false" not in r["Kernel_Name"]:
                 continue
@@ -140,8 +154,11 @@ def main():
     rates, classes_dir, out_json = sys.argv[1], sys.argv[2], sys.argv[3]
     isa = sys.argv[4] if len(sys.argv) > 4 and sys.argv[4] else build_isa()
     samples = float(sys.argv[5]) if len(sys.argv) > 5 else 250e6
+    config = sys.argv[6] if len(sys.argv) > 6 else "c4"
+    clock_hz = float(sys.argv[7]) * 1e9 if len(sys.argv) > 7 and sys.argv[7] else CLOCK_HZ
+    symbol = SYMBOLS[config]
     costs = measured_costs(rates)
-    ops = static_opcodes(isa)
+    ops = static_opcodes(isa, symbol)
     per_class = collections.defaultdict(lambda: [0, 0.0])   # static count, static count x cost
     for op, n in ops.items():
         c = class_of(op)
@@ -158,18 +175,18 @@ def main():
         avg = sw / sc if sc else costs.get("v_min3_f32", 4.2)
         demand += n * avg
         rows[c] = {"count_per_launch": n, "count_per_sample": n / samples, "cycles_each": avg, "static_opcodes": sc}
-    kernel_ns = pmc["kernel_ns_c4_1"]
-    cap = SIMDS * CLOCK_HZ * kernel_ns * 1e-9
+    kernel_ns = pmc["kernel_ns_pass1"]
+    cap = SIMDS * clock_hz * kernel_ns * 1e-9
     res = {
         "model": "sum over PMC classes of (dynamic count x static-mix mean of the measured per-opcode issue cost)",
-        "clock_hz": CLOCK_HZ, "simds": SIMDS, "samples_per_launch": samples,
+        "clock_hz": clock_hz, "simds": SIMDS, "samples_per_launch": samples,
         "valu_insts_per_launch": total, "valu_issue_cycles_per_launch": demand,
         "valu_issue_cycles_per_sample": demand / samples,
         "kernel_ns_pmc_pass": kernel_ns,
         "valu_issue_frac_pmc_pass": demand / cap,
         "uniform_2cyc_frac": total * 2 / cap, "uniform_4cyc_frac": total * 4 / cap,
         "classes": rows, "costs_measured": costs,
-        "isa_symbol": SYMBOL,
+        "isa_symbol": symbol, "config": config,
     }
     with open(out_json, "w") as f:
         json.dump(res, f, indent=1)
