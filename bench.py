@@ -26,7 +26,7 @@ Prints ONE JSON line (rank 0) with
     achieved = the wave-level VALU instructions of one launch (SQ_INSTS_VALU per
     sample from the committed rocprofv3 pass, profiles/r<NN>/traffic.json, for this
     very library build) over the kernel's live HIP-event time; peak = the rate 1,024
-    SIMDs x 2.4 GHz sustain on THIS kernel's instruction mix: each PMC instruction
+    SIMDs x 2.4 GHz (peak engine clock) sustain on THIS kernel's instruction mix: each PMC instruction
     class charged its microbenchmarked issue cost (tools/valu_issue_model.py:
     ~2.4 cycles for f32 add/mul, integer add, logic and moves, ~4.2 for FMA,
     min/max, compares, selects, shifts and 64-bit ops, ~8.2 for transcendentals).
@@ -360,9 +360,10 @@ def main():
             roof["frac_uniform_2cyc"] = vi / avg_kernel_s / VALU_PEAK
             cpi = prof.get("valu_issue_cycles_per_instr")
             if cpi:
-                clock = prof.get("effective_clock_ghz") or CLOCK_GHZ   # the kernel's clock in the PMC pass
-                peak = SIMDS * clock * 1e9 / cpi
-                roof["clock_ghz"] = clock
+                # at the 2.4 GHz peak engine clock: the PMC passes saw 2.30-2.36 GHz, so this
+                # frac is a lower bound of the share of issue capacity the kernel uses
+                peak = SIMDS * CLOCK_GHZ * 1e9 / cpi
+                roof["clock_ghz_pmc_pass"] = prof.get("effective_clock_ghz")
                 roof["valu_issue_cycles_per_instr"] = cpi
                 roof["peak"] = peak / 1e9
                 roof["frac"] = vi / avg_kernel_s / peak
