@@ -965,15 +965,17 @@ __device__ __forceinline__ CamView load_camera(const CamV4 *lds) {
 }
 
 // ------------------------------------------------------- lockstep primitives
-// Tests primitives [first, first + count) of an LDS copy (4 float4 each, the HBM
-// record) against every lane's ray in lockstep: the primitive, its kind and its
-// instance are the same in all lanes (broadcast reads, scalar branches), so only
+// Tests primitives [first, first + count) (4 float4 each, read through the scalar
+// cache: P is a constant-address-space pointer and q is uniform, so the records land
+// in SGPRs) against every lane's ray in lockstep: the primitive, its kind and its
+// instance are the same in all lanes (scalar loads and branches), so only
 // the kind's own test runs and no lane idles behind another's traversal.  Lanes
 // with `in` false compute but keep nothing.  kPerPrimInst: each primitive's own
 // instance chain (pre-scan); otherwise the caller transformed `r` for the group.
 typedef __attribute__((address_space(3))) const F4v LdsScan;
-template <bool kCount, bool kInst, bool kPerPrimInst>
-__device__ __forceinline__ void lockstep_prims(const LdsScan *P, int first, int count, const float4 *insts,
+typedef __attribute__((address_space(4))) const F4v ConstF4;   // uniform index: scalar (SMEM) loads
+template <bool kCount, bool kInst, bool kPerPrimInst, class PT>
+__device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const float4 *insts,
                                                const Ray &r, float tmin, bool in, int group_inst, float &best_t,
                                                int &best_key, uint32_t &best_prim, Counters &cnt) {
     for (int q = first; q < first + count; ++q) {
