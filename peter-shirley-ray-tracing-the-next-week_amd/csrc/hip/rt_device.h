@@ -272,7 +272,10 @@ __device__ __forceinline__ int rect_axis(int kind) { return 4 - kind; }
 // the moving-sphere centre and a sphere's second root stay behind branches.
 // kInst = false: the scene has no instance chains (the host knows), so the kernel
 // carries no instance code at all (fewer registers live across the leaf tests).
-template <bool kInst = true>
+// kKinds: what the WAVE tests in this call — 1 spheres only, 2 rects only, 3 both
+// (the caller ballots the kinds): a uniform wave skips the other kind's terms
+// (sphere-only: no plane selects; rect-only: no quadratic and no square root).
+template <bool kInst = true, int kKinds = 3>
 __device__ __forceinline__ float prim_t_head(float4 g0, float4 mm, const float4 *P, const float4 *insts, uint32_t idx,
                                              const Ray &r0, float tmin, int &key, int &kind_out) {
     const int kind = fbits(mm.x) & 0xff;
@@ -281,11 +284,11 @@ __device__ __forceinline__ float prim_t_head(float4 g0, float4 mm, const float4 
     kind_out = kind | (kInst && inst >= 0 ? 0x100 : 0);
     Ray r = r0;
     if (kInst && inst >= 0) r = to_object(insts, inst, r0);
-    const bool sph = kind <= RT_PRIM_MOVING_SPHERE;
+    const bool sph = kKinds == 1 ? true : (kKinds == 2 ? false : kind <= RT_PRIM_MOVING_SPHERE);
     key = sph ? order : -1 - order;   // a later rect wins a tie (aarect.h:52 accepts t == t_max)
     // sphere.h:25-52 (moving: the centre at r.time, sphere.h:81-83)
     V3 c = mk(g0.x, g0.y, g0.z);
-    if (kind == RT_PRIM_MOVING_SPHERE) c = msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time);
+    if (kKinds != 2 && kind == RT_PRIM_MOVING_SPHERE) c = msphere_center(g0, P[idx * 4 + 2], P[idx * 4 + 3], r.time);
     const V3 oc = sub(r.o, c);
     const float a = dot(r.d, r.d);
     const float b = dot(oc, r.d);

@@ -29,6 +29,8 @@
 // Arithmetic follows the reference's float/double promotions; the file is compiled
 // with -ffp-contract=off so no FMA is introduced where the reference has none (the
 // BVH slab test, which decides nothing about the result, uses explicit fmaf).
+#include <type_traits>
+
 #include "rt_device.h"
 
 namespace {
@@ -315,19 +317,30 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                             const uint32_t ib = two ? ia + 1 : ia;
                             const float4 ga = A.prims[ia * 4 + 0], ma = A.prims[ia * 4 + 1];
                             const float4 gb = A.prims[ib * 4 + 0], mb = A.prims[ib * 4 + 1];
-                            int key, kind;
-                            float t = prim_t_head<kInst>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
-                            if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                            if (t < best_t || (t == best_t && key < best_key)) {
-                                best_t = t; best_key = key; best_prim = ia;
-                            }
-                            if (two) {
-                                t = prim_t_head<kInst>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
+                            auto test_pair = [&](auto kinds) {
+                                constexpr int kK = decltype(kinds)::value;
+                                int key, kind;
+                                float t = prim_t_head<kInst, kK>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
                                 if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
                                 if (t < best_t || (t == best_t && key < best_key)) {
-                                    best_t = t; best_key = key; best_prim = ib;
+                                    best_t = t; best_key = key; best_prim = ia;
                                 }
-                            }
+                                if (two) {
+                                    t = prim_t_head<kInst, kK>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
+                                    if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
+                                    if (t < best_t || (t == best_t && key < best_key)) {
+                                        best_t = t; best_key = key; best_prim = ib;
+                                    }
+                                }
+                            };
+                            // the kinds the wave tests in this pass: a wave of spheres only or of
+                            // rects only runs that kind's test alone (final(): most passes)
+                            const bool ra = (fbits(ma.x) & 0xff) > RT_PRIM_MOVING_SPHERE;
+                            const bool rb = two && (fbits(mb.x) & 0xff) > RT_PRIM_MOVING_SPHERE;
+                            const bool sb = two && !rb;
+                            if (wballot(ra || rb) == 0ull) test_pair(std::integral_constant<int, 1>());
+                            else if (wballot(!ra || sb) == 0ull) test_pair(std::integral_constant<int, 2>());
+                            else test_pair(std::integral_constant<int, 3>());
                         }
                     }
                     if (node == RT_EMPTY_CHILD) phase = PH_READY;   // stack empty too (popped above)
