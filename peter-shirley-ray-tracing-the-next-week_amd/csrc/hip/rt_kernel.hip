@@ -49,6 +49,9 @@ namespace {
 #define RT_DESCEND_STEPS 2
 #endif
 
+// Pre-made sample starts per wave (refill): one per lane.
+#define RT_PRE 64
+
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -78,12 +81,19 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ CamV4 lds_cam[6];
+    // per wave: the next RT_PRE work items' sample starts, made 64 at a time (refill)
+    __shared__ uint32_t lds_pre_item[kBlock / 64][RT_PRE];
+    __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
+    __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
     uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(lds_dyn + 4 * RT_LDS_NODE_CAP) +
                                (threadIdx.x >> 6) * (uint32_t)A.stack_depth * 64u + lane
                          : &lds_stack[kMode ? 0 : threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
+    uint32_t *pre_item = lds_pre_item[threadIdx.x >> 6];
+    uint64_t *pre_key = lds_pre_key[threadIdx.x >> 6];
+    float2 *pre_uv = lds_pre_uv[threadIdx.x >> 6];
     // the media records are read from LDS (one broadcast read per medium)
     load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) store_camera(A, lds_cam);
@@ -108,9 +118,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     const LdsNodes lnodes{(const LdsF4 *)lds_dyn};
 
     const uint64_t skey = seed_key(A.seed);   // per-launch part of the sample keys
-    // wave-uniform claim pool
+    // wave-uniform claim pool, and the pre-made sample starts [pre_head, pre_head + pre_count)
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
+    uint32_t pre_head = 0, pre_count = 0;
 
     // lane state: work item, path, traversal
     uint32_t item = 0xFFFFFFFFu;
@@ -123,7 +134,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     V3 beta = mk(1, 1, 1);
     int depth = 0;
     Rng g; g.ctr = 0; g.mkey = 0;
-    uint32_t px = 0, py = 0;
+    // this lane's pre-made sample start, taken by retire_and_claim for camera_begin
+    // (read out at once: a refill later in the same claim reuses the slots)
+    bool pre_have = false;
+    uint64_t pre_k = 0;
+    float2 pre_cuv = make_float2(0.f, 0.f);
     uint32_t node = 0;
     int sp = 0;
     float best_t = RT_FLT_MAX;
@@ -153,8 +168,43 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (kCount) cnt.segments++;
     };
 
-    // retire a finished work item (its sum to the slab), claim new ones for the lanes
-    // without work from the wave's pool (one global atomic per A.claim items)
+    // Sample starts are made for 64 work items at once, by all lanes of the wave
+    // (refill): each item's pixel, sample key, medium-stream key and the two jitter
+    // draws (main.cpp:305-306) — four of a new sample's five hashes, which a lane
+    // starting a sample alone would run at the few-lane occupancy of path
+    // regeneration.  They wait in the wave's LDS slots until a lane takes one.
+    auto refill = [&]() {   // all 64 lanes; wave-uniform outcome
+        if (pool_next == pool_end) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(A.counter, A.claim);
+            base = __shfl(base, 0);
+            if (base >= A.nitems) { exhausted = true; return; }
+            pool_next = base;
+            pool_end = min(base + A.claim, A.nitems);
+        }
+        const uint32_t n = min(64u, pool_end - pool_next);
+        if (lane < n) {
+            const uint32_t it = pool_next + lane;
+            const uint32_t c = it / A.npix;
+            const uint32_t xy = A.job_xy[it - c * A.npix];
+            const int x = (int)(xy & 0xFFFFu), j = A.ny - 1 - (int)(xy >> 16);
+            const uint64_t K = sample_key(skey, (uint32_t)(j * A.nx + x), c * (uint32_t)A.chunk + A.sample_offset);
+            // main.cpp:305-306; A.rnx = RN(1/float(nx)) from the host (div_rn)
+            const float cu = div_rn((float)((double)x + u48(mix64(K + kGamma))), (float)A.nx, A.rnx);
+            const float cv = div_rn((float)((double)j + u48(mix64(K + 2 * kGamma))), (float)A.ny, A.rny);
+            pre_item[lane] = it;
+            pre_key[lane] = K;
+            pre_uv[lane] = make_float2(cu, cv);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pre_head = 0;
+        pre_count = n;
+        pool_next += n;
+    };
+    // retire a finished work item (its sum to the slab), hand the lanes without work
+    // the next pre-made sample starts (one global atomic per A.claim items)
     auto retire_and_claim = [&]() {
         if (phase == PH_IDLE && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
             A.slab[item] = make_float4(part.x, part.y, part.z, 0.f);
@@ -162,31 +212,27 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
         bool need = phase == PH_IDLE && !finished && item == 0xFFFFFFFFu;
         uint64_t need_mask = wballot(need);
-        while (need_mask != 0ull && !exhausted) {
-            if (pool_next == pool_end) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(A.counter, A.claim);
-                base = __shfl(base, 0);
-                if (base >= A.nitems) { exhausted = true; break; }
-                pool_next = base;
-                pool_end = min(base + A.claim, A.nitems);
+        while (need_mask != 0ull) {
+            if (pre_count == 0) {
+                if (!exhausted) refill();
+                if (pre_count == 0) break;
             }
-            uint32_t avail = pool_end - pool_next;
-            uint32_t rank = lanes_below(need_mask);
-            if (need && rank < avail) {
-                item = pool_next + rank;
+            const uint32_t rank = lanes_below(need_mask);
+            if (need && rank < pre_count) {
+                const uint32_t e = pre_head + rank;
+                item = pre_item[e];
+                pre_k = pre_key[e];
+                pre_cuv = pre_uv[e];
+                pre_have = true;
                 need = false;
-                uint32_t c = item / A.npix;
-                uint32_t p = item - c * A.npix;
-                uint32_t xy = A.job_xy[p];
-                px = xy & 0xFFFFu;
-                py = xy >> 16;
+                const uint32_t c = item / A.npix;
                 s_cur = (int)(c * (uint32_t)A.chunk);
                 s_end = min(s_cur + A.chunk, A.ns);
                 part = mk(0, 0, 0);
             }
-            uint32_t wanted = (uint32_t)__popcll(need_mask);
-            pool_next += min(wanted, avail);
+            const uint32_t took = min((uint32_t)__popcll(need_mask), pre_count);
+            pre_head += took;
+            pre_count -= took;
             need_mask = wballot(need);
         }
         if (need) finished = true;
@@ -195,11 +241,21 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // jitter, then (after the lens-disk point) the ray
     auto camera_begin = [&](bool starting, float &cu_, float &cv_) {
         if (starting) {
-            int j = A.ny - 1 - (int)py;
-            g.start(sample_key(skey, (uint32_t)(j * A.nx + (int)px), (uint32_t)s_cur + A.sample_offset));
-            // main.cpp:305-306; A.rnx = RN(1/float(nx)) from the host (div_rn)
-            cu_ = div_rn((float)((double)(int)px + g.next()), (float)A.nx, A.rnx);
-            cv_ = div_rn((float)((double)j + g.next()), (float)A.ny, A.rny);
+            if (pre_have) {   // a work item's first sample: made by refill
+                g.start(pre_k);
+                g.skip();
+                g.skip();   // the two jitter draws
+                cu_ = pre_cuv.x;
+                cv_ = pre_cuv.y;
+                pre_have = false;
+            } else {            // a further sample of a multi-sample work item (chunk > 1)
+                const uint32_t c = item / A.npix;
+                const uint32_t xy = A.job_xy[item - c * A.npix];
+                const int px = (int)(xy & 0xFFFFu), j = A.ny - 1 - (int)(xy >> 16);
+                g.start(sample_key(skey, (uint32_t)(j * A.nx + px), (uint32_t)s_cur + A.sample_offset));
+                cu_ = div_rn((float)((double)px + g.next()), (float)A.nx, A.rnx);
+                cv_ = div_rn((float)((double)j + g.next()), (float)A.ny, A.rny);
+            }
         }
     };
     auto camera_finish = [&](bool starting, float cu_, float cv_, V3 disk) {
@@ -531,5 +587,6 @@ extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int 
 
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
-    return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16) + 256;
+    return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 +
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (4 + 8 + 8)) + 256;
 }
