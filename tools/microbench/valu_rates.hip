@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <algorithm>
+
 #define N_ITER 4096
 // shader clock of the run: block 0's first wave stamps s_memtime (shader cycles) and
 // s_memrealtime (100 MHz) at its start and end (MI355X_MICROARCH.md, in-kernel clock);
@@ -216,16 +218,23 @@ int main() {
     hipEventCreate(&a);
     hipEventCreate(&b);
     for (auto &k : ks) {
-        hipLaunchKernelGGL(k.k, dim3(blocks), dim3(256), 0, 0, out, 0x9E3779B9u);
-        hipEventRecord(a);
-        hipLaunchKernelGGL(k.k, dim3(blocks), dim3(256), 0, 0, out, 0x9E3779B9u);
-        hipEventRecord(b);
-        hipEventSynchronize(b);
-        float ms = 0;
-        hipEventElapsedTime(&ms, a, b);
-        unsigned long long st[4];
-        hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st);
-        const double mhz = (double)(st[2] - st[0]) / (double)(st[3] - st[1]) * 100.0;   // shader cycles per 10 ns
+        hipLaunchKernelGGL(k.k, dim3(blocks), dim3(256), 0, 0, out, 0x9E3779B9u);   // warm-up
+        double mss[5], mhzs[5];
+        for (int rep = 0; rep < 5; ++rep) {   // median of 5 launches
+            hipEventRecord(a);
+            hipLaunchKernelGGL(k.k, dim3(blocks), dim3(256), 0, 0, out, 0x9E3779B9u);
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms = 0;
+            hipEventElapsedTime(&ms, a, b);
+            unsigned long long st[4];
+            hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof st);
+            mss[rep] = ms;
+            mhzs[rep] = (double)(st[2] - st[0]) / (double)(st[3] - st[1]) * 100.0;   // shader cycles per 10 ns
+        }
+        std::sort(mss, mss + 5);
+        std::sort(mhzs, mhzs + 5);
+        const double ms = mss[2], mhz = mhzs[2];
         const double insts_per_simd = (double)waves_per_simd * N_ITER * 32;
         const double cyc = ms * 1e-3 * clk * 1e3 / insts_per_simd;
         printf("%-18s %8.3f ms  %6.2f cycles per wave-instruction per SIMD (clock %d MHz)  measured clock %.0f MHz: %.2f cycles\n",
