@@ -82,7 +82,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ CamV4 lds_cam[6];
     // per wave: the next RT_PRE work items' sample starts, made 64 at a time (refill)
-    __shared__ uint32_t lds_pre_item[kBlock / 64][RT_PRE];
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
@@ -91,7 +90,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                                (threadIdx.x >> 6) * (uint32_t)A.stack_depth * 64u + lane
                          : &lds_stack[kMode ? 0 : threadIdx.x >> 6][0][lane];
     CoopSlot *slots = lds_slots[threadIdx.x >> 6];
-    uint32_t *pre_item = lds_pre_item[threadIdx.x >> 6];
     uint64_t *pre_key = lds_pre_key[threadIdx.x >> 6];
     float2 *pre_uv = lds_pre_uv[threadIdx.x >> 6];
     // the media records are read from LDS (one broadcast read per medium)
@@ -121,7 +119,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // wave-uniform claim pool, and the pre-made sample starts [pre_head, pre_head + pre_count)
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
-    uint32_t pre_head = 0, pre_count = 0;
+    // entry e holds item pre_base + e, of sample chunk pre_c0 (+1 from entry pre_split on)
+    uint32_t pre_head = 0, pre_count = 0, pre_base = 0, pre_c0 = 0, pre_split = 0;
 
     // lane state: work item, path, traversal
     uint32_t item = 0xFFFFFFFFu;
@@ -192,7 +191,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             // main.cpp:305-306; A.rnx = RN(1/float(nx)) from the host (div_rn)
             const float cu = div_rn((float)((double)x + u48(mix64(K + kGamma))), (float)A.nx, A.rnx);
             const float cv = div_rn((float)((double)j + u48(mix64(K + 2 * kGamma))), (float)A.ny, A.rny);
-            pre_item[lane] = it;
             pre_key[lane] = K;
             pre_uv[lane] = make_float2(cu, cv);
         }
@@ -201,6 +199,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         pre_head = 0;
         pre_count = n;
+        pre_base = pool_next;
+        pre_c0 = pool_next / A.npix;
+        pre_split = (pre_c0 + 1) * A.npix - pool_next;
         pool_next += n;
     };
     // retire a finished work item (its sum to the slab), hand the lanes without work
@@ -220,12 +221,13 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const uint32_t rank = lanes_below(need_mask);
             if (need && rank < pre_count) {
                 const uint32_t e = pre_head + rank;
-                item = pre_item[e];
+                item = pre_base + e;
                 pre_k = pre_key[e];
                 pre_cuv = pre_uv[e];
                 pre_have = true;
                 need = false;
-                const uint32_t c = item / A.npix;
+                // a refill's 64 items cross at most one chunk boundary when npix >= 64
+                const uint32_t c = A.npix >= 64 ? pre_c0 + (e >= pre_split ? 1u : 0u) : item / A.npix;
                 s_cur = (int)(c * (uint32_t)A.chunk);
                 s_end = min(s_cur + A.chunk, A.ns);
                 part = mk(0, 0, 0);
@@ -588,5 +590,5 @@ extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int 
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 +
-                 (RT_LDS_BLOCK / 64) * RT_PRE * (4 + 8 + 8)) + 256;
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8)) + 256;
 }
