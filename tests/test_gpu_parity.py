@@ -136,6 +136,19 @@ def test_tile_decomposition_is_bitwise_invariant():
     assert np.array_equal(full.view(np.uint32), quad.view(np.uint32))
 
 
+def test_small_tiles_match_the_full_render():
+    """Jobs of fewer pixels than a wave has lanes: one refill of sample starts then
+    spans several sample chunks (1x1, 5x3, 7x9 = 63 and 8x8 = 64 pixels; the
+    kernel's work-claim path for npix < 64), and the tile must still be bitwise the
+    same pixels of the full render."""
+    nx, ny, ns = 40, 24, 12
+    for chunk in (1, 16):   # one sample per work item (default), and multi-sample items
+        full = gpu_render("final", nx, ny, ns, seed=9, chunk=chunk)
+        for (x0, y0, w, h) in [(3, 4, 1, 1), (10, 7, 5, 3), (20, 10, 7, 9), (0, 16, 8, 8)]:
+            t = gpu_render("final", nx, ny, ns, seed=9, chunk=chunk, rect=(x0, y0, w, h))
+            assert np.array_equal(full[y0:y0 + h, x0:x0 + w].view(np.uint32), t.view(np.uint32)), (chunk, x0, y0, w, h)
+
+
 def test_rank_sharding_gathers_to_single_gpu_image():
     """Rank layouts (16x16 tiles diagonal or hashed, the pixel interleave) over R
     emulated ranks, packed per rank as the
