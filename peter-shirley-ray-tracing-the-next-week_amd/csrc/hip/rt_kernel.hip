@@ -457,6 +457,26 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
         camera_finish(starting, cu_, cv_, pt);
         mark(3);
+#ifdef RT_PROBE_VALU
+#if RT_PROBE_VALU == 1
+#define RT_PROBE_OP "v_add_f32 %0, %0, %1"
+#elif RT_PROBE_VALU == 2
+#define RT_PROBE_OP "v_max_f32 %0, %0, %1"
+#else
+#define RT_PROBE_OP "v_fma_f32 %0, %0, %1, %1"
+#endif
+        {   // timing probe only: 64 independent extra VALU instructions of one opcode per
+            // wave iteration, on registers that feed nothing (in-situ costs)
+            float q0 = (float)lane, q1 = q0 + 1.f, q2 = q0 + 2.f, q3 = q0 + 3.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                asm volatile(RT_PROBE_OP : "+v"(q0) : "v"(q1));
+                asm volatile(RT_PROBE_OP : "+v"(q1) : "v"(q2));
+                asm volatile(RT_PROBE_OP : "+v"(q2) : "v"(q3));
+                asm volatile(RT_PROBE_OP : "+v"(q3) : "v"(q0));
+            }
+        }
+#endif
     }
     if (kProf && lane == 0)
         for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_CNT_N + k], (unsigned long long)prof[k]);
