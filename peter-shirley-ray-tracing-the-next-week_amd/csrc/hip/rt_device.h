@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "rt_layout.h"
 #include "rt_log_table.h"
@@ -497,13 +498,22 @@ __device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, fl
 // ------------------------------------------------------------ BVH node step
 // Per-ray slab-test constants: 1/d (padded boxes need no exact division) and
 // -o/d, duplicated into packed pairs for v_pk_fma_f32.
-struct Slab { F2 ix, iy, iz, nox, noy, noz; float tmin; };
+// LDS nodes (LdsNodes::load_signed): lx/ly/lz are the byte offsets of the ray's
+// near planes in the axis' plane (+4 when the direction is negative: hi before lo).
+#ifndef RT_LDS_SIGNED
+#define RT_LDS_SIGNED 1
+#endif
+struct Slab { F2 ix, iy, iz, nox, noy, noz; float tmin; uint32_t lx, ly, lz, fx, fy, fz; };
 __device__ __forceinline__ Slab make_slab(const Ray &r, float tmin) {
     const float ix = __builtin_amdgcn_rcpf(r.d.x), iy = __builtin_amdgcn_rcpf(r.d.y), iz = __builtin_amdgcn_rcpf(r.d.z);
     Slab s;
     s.ix = F2{ix, ix}; s.iy = F2{iy, iy}; s.iz = F2{iz, iz};
     s.nox = F2{-r.o.x * ix, -r.o.x * ix}; s.noy = F2{-r.o.y * iy, -r.o.y * iy}; s.noz = F2{-r.o.z * iz, -r.o.z * iz};
     s.tmin = tmin;
+    s.lx = ((__float_as_uint(ix) >> 31) << 2) + RT_LDS_NODE_CAP * 16;
+    s.ly = ((__float_as_uint(iy) >> 31) << 2) + 2 * RT_LDS_NODE_CAP * 16;
+    s.lz = ((__float_as_uint(iz) >> 31) << 2) + 3 * RT_LDS_NODE_CAP * 16;
+    s.fx = s.lx ^ 4u; s.fy = s.ly ^ 4u; s.fz = s.lz ^ 4u;
     return s;
 }
 // entry distance of one child box, +inf if the ray misses it (or, kSlots, the slot
@@ -557,11 +567,45 @@ struct GlobalNodes {
     __device__ __forceinline__ const float4 *ptr8(uint32_t n) const { return p + n * 16; }
     __device__ __forceinline__ const float4 *ptr8q(uint32_t n) const { return p + n * 8; }
 };
+// LDS planes, per axis (RT_LDS_SIGNED): plane 0 holds the child references (first,
+// so that their read needs no address add: the LDS base fits the immediate offset),
+// plane 1 + a (lo0, hi0, lo1, hi1) of axis a for both children.  A lane reads its near planes at
+// +0 or +4 by the sign of its direction (Slab::lx..lz) and its far planes at the
+// other word: near/far come out of the load, not out of a min and a max per axis
+// and child (12 VALU per node step for 6 address adds).  Without RT_LDS_SIGNED the
+// planes are the node's 4 float4 (rt_layout.h).
 struct LdsNodes {   // node references are byte offsets (n * 16) into the planes
     const LdsF4 *p;
     __device__ __forceinline__ void load2(uint32_t n, float4 &b0, float4 &b1, float4 &b2, float4 &cf) const {
         const LdsF4 *N = (const LdsF4 *)((__attribute__((address_space(3))) const char *)p + n);
         b0 = f4(N[0]); b1 = f4(N[RT_LDS_NODE_CAP]); b2 = f4(N[2 * RT_LDS_NODE_CAP]); cf = f4(N[3 * RT_LDS_NODE_CAP]);
+    }
+    // the six plane offsets become LDS addresses once per round, opaque to the
+    // compiler, which would otherwise re-split base + plane + sign per node step
+    // (11 address adds per node instead of 6)
+    static __device__ __forceinline__ uint32_t opaque(uint32_t x) { asm("" : "+v"(x)); return x; }
+    __device__ __forceinline__ void prepare(Slab &s) const {
+        const uint32_t b = (uint32_t)(size_t)p;
+        s.lx = opaque(b + s.lx); s.ly = opaque(b + s.ly); s.lz = opaque(b + s.lz);
+        s.fx = opaque(b + s.fx); s.fy = opaque(b + s.fy); s.fz = opaque(b + s.fz);
+    }
+    // after prepare()
+    __device__ __forceinline__ void load_signed(uint32_t n, const Slab &s, F2 &nx, F2 &ny, F2 &nz, F2 &fx, F2 &fy, F2 &fz,
+                                                uint32_t &c0, uint32_t &c1) const {
+        typedef __attribute__((address_space(3))) const float LdsF;
+        typedef __attribute__((address_space(3))) const char LdsC;
+        auto pair = [&](uint32_t a) {   // (child 0, child 1) at one address: one ds_read2_b32
+            const LdsF *q = (const LdsF *)(size_t)(n + a);
+            return F2{q[0], q[2]};
+        };
+        nx = pair(s.lx); fx = pair(s.fx);
+        ny = pair(s.ly); fy = pair(s.fy);
+        nz = pair(s.lz); fz = pair(s.fz);
+        typedef unsigned U2v __attribute__((ext_vector_type(2)));
+        const __attribute__((address_space(3))) U2v *C =
+            (const __attribute__((address_space(3))) U2v *)((LdsC *)p + n);
+        const U2v c = *C;
+        c0 = c.x; c1 = c.y;
     }
     __device__ __forceinline__ const float4 *ptr4(uint32_t) const { return nullptr; }   // wide BVHs stay in HBM
     __device__ __forceinline__ const float4 *ptr8(uint32_t) const { return nullptr; }
@@ -598,7 +642,24 @@ __device__ __forceinline__ uint32_t wide8_tail(const float k[8], const uint32_t 
 template <int kWidth, class Nodes>
 __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, const Slab &s, float best_t, uint32_t *stk,
                                               int &sp) {
-    if (kWidth == 2) {   // rt_dnode2
+    if constexpr (kWidth == 2 && RT_LDS_SIGNED && std::is_same<Nodes, LdsNodes>::value) {
+        F2 nx, ny, nz, fx, fy, fz;
+        uint32_t c0, c1;
+        src.load_signed(node, s, nx, ny, nz, fx, fy, fz, c0, c1);
+        // both children per packed FMA: .x child 0, .y child 1
+        const F2 an = pk_fma(nx, s.ix, s.nox), bn = pk_fma(ny, s.iy, s.noy), en = pk_fma(nz, s.iz, s.noz);
+        const F2 af = pk_fma(fx, s.ix, s.nox), bf = pk_fma(fy, s.iy, s.noy), ef = pk_fma(fz, s.iz, s.noz);
+        const float tn0 = imax(vmax3(an.x, bn.x, en.x), s.tmin), tf0 = imin(vmin3(af.x, bf.x, ef.x), best_t);
+        const float tn1 = imax(vmax3(an.y, bn.y, en.y), s.tmin), tf1 = imin(vmin3(af.y, bf.y, ef.y), best_t);
+        const bool h0 = tn0 <= tf0, h1 = tn1 <= tf1;
+        const bool lt = tn1 < tn0;
+        const bool second = h1 & (!h0 | lt);
+        const uint32_t nearc = second ? c1 : (h0 ? c0 : RT_EMPTY_CHILD), farc = second ? c0 : c1;
+        stk[sp * 64] = farc;
+        const int sp0 = h0 ? sp + 1 : sp;
+        sp = h1 ? sp0 : sp;
+        return nearc;
+    } else if (kWidth == 2) {   // rt_dnode2
         float4 b0, b1, b2, cf;
         src.load2(node, b0, b1, b2, cf);
         const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);

@@ -105,10 +105,18 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
             cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : c0 << 4);
             cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : c1 << 4);
+#if RT_LDS_SIGNED
+            // the references, then per-axis planes (LdsNodes::load_signed): (lo0, hi0, lo1, hi1) of x, y, z
+            lds_dyn[i] = cf;
+            lds_dyn[i + RT_LDS_NODE_CAP] = make_float4(b0.x, b0.y, b1.z, b1.w);
+            lds_dyn[i + 2 * RT_LDS_NODE_CAP] = make_float4(b0.z, b0.w, b2.x, b2.y);
+            lds_dyn[i + 3 * RT_LDS_NODE_CAP] = make_float4(b1.x, b1.y, b2.z, b2.w);
+#else
             lds_dyn[i] = b0;
             lds_dyn[i + RT_LDS_NODE_CAP] = b1;
             lds_dyn[i + 2 * RT_LDS_NODE_CAP] = b2;
             lds_dyn[i + 3 * RT_LDS_NODE_CAP] = cf;
+#endif
         }
     }
     __syncthreads();
@@ -360,8 +368,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 if (__popcll(wballot(phase == PH_READY)) >= RT_READY_BATCH) break;
                 if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
-                    const Slab sl = make_slab(r, A.tmin);
+                    Slab sl = make_slab(r, A.tmin);
                     uint32_t pleaf;
+                    if constexpr (kLds && RT_LDS_SIGNED && kWidth == 2) lnodes.prepare(sl);
                     if constexpr (kLds)
                         pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt);
                     else
