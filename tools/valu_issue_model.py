@@ -132,8 +132,12 @@ def pmc_counts(classes_dir):
         path = os.path.join(classes_dir, sub, "run_counter_collection.csv")
         if not os.path.exists(path):
             path = os.path.join(classes_dir, "pmc_classes_%s.csv" % sub[-1])
+        first = None   # the first timed launch (c5 on one GPU: two launches of different sizes)
         for r in csv.DictReader(open(path)):
             if "rt_megakernel<false, false" not in r["Kernel_Name"]:
+                continue
+            first = r["Dispatch_Id"] if first is None else first
+            if r["Dispatch_Id"] != first:
                 continue
             tot[r["Counter_Name"]] = float(r["Counter_Value"])
             tot["kernel_ns_" + sub] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
