@@ -551,9 +551,8 @@ __device__ __forceinline__ void cas(float &ka, uint32_t &ca, float &kb, uint32_t
 // builder bounds sp by RT_STACK_DEPTH - 1), return the nearest (or empty).
 // Where a node step reads its node.  BVH2 nodes are 4 float4 (rt_layout.h); the
 // global reader fetches them from HBM (L1/L2), the LDS reader from the workgroup's
-// copy, stored as 4 planes of RT_LDS_NODE_CAP float4 (plane k holds float4 k of every
-// node) so one address register serves the 4 ds_read_b128 (immediate offsets) and
-// lanes reading different nodes spread over 16 bank windows instead of 4.
+// copy, stored as 4 planes of RT_LDS_NODE_CAP float4 so that lanes reading different
+// nodes spread over 16 bank windows instead of 4 (the plane contents: load_signed).
 typedef float F4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const F4v LdsF4;
 __device__ __forceinline__ float4 f4(F4v v) { return make_float4(v.x, v.y, v.z, v.w); }
