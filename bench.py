@@ -386,7 +386,7 @@ def main():
     if rank == 0:
         res = {
             "metric": METRIC if cfg == "c4" else
-            f"Msamples/s (pixels×spp/s) + achieved HBM GB/s, {scene_name}() {w1}×{h1}×{CONFIGS[cfg][3]}spp",
+            f"Msamples/s (pixels×spp/s) + achieved HBM GB/s, {scene_name}() {w1}×{h1}×{spp}spp",
             "value": value,
             "unit": "Msamples/s",
             "n_gpus": world,
