@@ -14,12 +14,16 @@ Workloads (BASELINE.json configs):
       strong scaling, total work fixed (the config BASELINE quotes for 8 GPUs).
       The pixels are interleaved over the ranks (N = a x b, rank (ry, rx) renders
       x = rx mod a, y = ry mod b: a sub-sampled copy of the whole view, so every
-      rank's expected cost is the same), then ONE gather to rank 0: `--gather
-      torch` (default: torch.distributed.gather, backend "nccl" = RCCL) or
-      `--gather native` (the C ABI's rt_dist_gather = ncclGather on its own RCCL
-      communicator, rccl.h:745).  `--dist-backend gloo` gathers through host memory
-      so the multi-rank path can be rehearsed with several ranks on one GPU.
+      rank's expected cost is the same), then ONE gather to rank 0: by default the
+      C ABI's rt_dist_gather (ncclGather on its own RCCL communicator, rccl.h:745,
+      over xGMI), or `--gather torch` (torch.distributed.gather).  `--dist-backend
+      gloo` gathers through host memory so the multi-rank path can be rehearsed with
+      several ranks on one GPU.
   --config c2 / c3 / c4 with N > 1: weak scaling, N x the 1-GPU pixels.
+
+Launch: under torchrun (WORLD_SIZE set; --gpus must equal it), or plain
+`python bench.py --gpus N`, which starts the N rank processes itself (launch_ranks).
+
 
 Prints ONE JSON line (rank 0) with
   roofline: the megakernel is bound by VALU instruction issue.
@@ -42,6 +46,7 @@ import glob
 import hashlib
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -222,9 +227,54 @@ def end_to_end(scene_name, cam, params, nx, ny, dev):
             "scene_create_ms": (t1 - t0) * 1e3, "render_ms": (t2 - t1) * 1e3, "readback_ms": (t3 - t2) * 1e3}
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` with no launcher around it: start N FRESH rank processes
+    (this interpreter has not touched the GPU: nothing before this call initialises
+    HIP) with the rendezvous environment torchrun would give them — the pattern of
+    examples/render_dist.cpp's fork-before-HIP launcher, as child processes, never an
+    exec of this one.  Rank 0's stdout is this process's stdout (the JSON line).  When
+    a rank fails, the others are terminated (a peer stuck in the rendezvous or in the
+    gather would otherwise wait forever) and the first failure's code is returned."""
+    port = _free_port()
+    procs = []
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env))
+        rc, live = 0, set(range(n))
+        while live:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    log(f"[launcher] rank {r} exited with {code}: stopping the other ranks")
+                    for q in live:
+                        procs[q].terminate()
+            time.sleep(0.05)
+        return rc
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher (WORLD_SIZE unset) bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="", choices=[""] + sorted(CONFIGS),
@@ -233,19 +283,41 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="samples per work item; 0 = the C ABI's default (1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ppm", default="")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
-    ap.add_argument("--gather", default="torch", choices=["torch", "native"],
-                    help="torch.distributed.gather, or the C ABI's rt_dist_gather (ncclGather on its own RCCL comm)")
+    ap.add_argument("--dump", default="", help="rank 0 saves the last step's float image (.npy) here")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo rehearses several ranks on one GPU")
+    ap.add_argument("--gather", default="auto", choices=["auto", "torch", "native"],
+                    help="the C ABI's rt_dist_gather (ncclGather on its own RCCL comm; auto with nccl), or "
+                         "torch.distributed.gather (auto with gloo)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        log(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RTNW_BENCH_FAIL_RANK") == str(rank):   # tests: a rank that dies before the rendezvous
+        log(f"[rank {rank}] RTNW_BENCH_FAIL_RANK: exiting")
+        sys.exit(3)
     ndev = torch.cuda.device_count()
     gpu = local % max(1, ndev)
     if world > 1:
-        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            if world > ndev:
+                log(f"bench.py: {world} ranks on {ndev} GPU(s): RCCL needs one GPU per rank "
+                    "(--dist-backend gloo rehearses several ranks on one GPU)")
+                sys.exit(2)
+            torch.cuda.set_device(gpu)
         dist.init_process_group(args.dist_backend)
+    if args.gather == "auto":
+        args.gather = "native" if args.dist_backend == "nccl" else "torch"
+    if args.gather == "native" and args.dist_backend != "nccl" and world > 1:
+        log("bench.py: --gather native is an RCCL gather: it needs --dist-backend nccl")
+        sys.exit(2)
     dev = torch.device("cuda", gpu)
 
     cfg = args.config or ("c4" if world == 1 else "c5")
@@ -342,6 +414,17 @@ def main():
             "node_visits_per_ray": cst["node_visits"] / max(1.0, cst["segments"]),
             "prim_tests_per_ray": (cst["sphere_tests"] + cst["moving_sphere_tests"] + cst["rect_tests"])
             / max(1.0, cst["segments"]),
+            # SIMD efficiency per stage from the counting run: lane-level events over 64 x
+            # the wave-level trips that ran them (node steps, primitive tests, the
+            # cooperative rejection rounds' candidates)
+            "lane_efficiency": {
+                "node_steps": cst["node_visits"] / max(1.0, 64 * cst["wave_node_trips"]),
+                # leaf tests: every test minus one boundary-sphere test per medium
+                # evaluation (exact when each medium's boundary is one sphere: final())
+                "prim_tests": (cst["sphere_tests"] + cst["moving_sphere_tests"] + cst["rect_tests"]
+                               - cst["medium_tests"]) / max(1.0, 64 * cst["wave_prim_trips"]),
+                "coop_candidates": cst["lane_sphere_draw_trips"] / max(1.0, 64 * cst["wave_sphere_draw_trips"]),
+                "segments_per_wave_iteration": cst["segments"] / max(1.0, cst["wave_iterations"])},
             "note": "the scene is L2/L1-resident: HBM carries ~1% of peak, the kernel is VALU-issue bound "
                     "(DESIGN.md §5c).  achieved = SQ_INSTS_VALU per sample (committed rocprofv3 pass of this "
                     "library build) x samples / live kernel time; peak = 1024 SIMDs x 2.4 GHz / the mean "
@@ -372,7 +455,7 @@ def main():
             roof["traffic"] = tr
             roof["hbm_frac"] = tr / avg_kernel_s / (HBM_PEAK_GBS * 1e9)
 
-    if rank == 0 and args.ppm:
+    if rank == 0 and (args.ppm or args.dump):
         if world == 1:
             img = out[: nx * ny * 3].cpu().numpy().reshape(ny, nx, 3)
         else:   # the last timed step's gathered shares, unpacked on the root
@@ -380,8 +463,11 @@ def main():
             for r in range(world):
                 src = recv[r * n_max:(r + 1) * n_max] if native else gather_list[r]
                 rtnw.unpack_tiles(src[: all_counts[r]].cpu().numpy(), all_tiles[r], img)
-        with open(args.ppm, "wb") as f:
-            f.write(rtnw.ppm_text(rtnw.quantize(img)))
+        if args.ppm:
+            with open(args.ppm, "wb") as f:
+                f.write(rtnw.ppm_text(rtnw.quantize(img)))
+        if args.dump:
+            np.save(args.dump, img)
 
     if rank == 0:
         res = {

@@ -9,6 +9,7 @@
 // The launcher forks the N rank processes BEFORE anything touches the GPU (no exec);
 // rank 0 creates the RCCL unique id and passes it to the others through a pipe.
 // N defaults to the number of GPUs (RCCL needs one GPU per rank).
+#include <signal.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -51,6 +52,14 @@ int run_rank(const Options &o, int rank, int rfd, int wfd) {
     if (rt_device_count(&ndev) != RT_OK || ndev == 0) { std::fprintf(stderr, "no HIP device\n"); return 1; }
     const int device = rank % ndev;
 
+    // tests: a rank that fails after the id exchange but before joining the
+    // communicator, as a failed scene build would; its peers wait in ncclCommInitRank
+    // until the launcher stops them
+    const char *fail_rank = std::getenv("RTNW_DIST_FAIL_RANK");
+    if (fail_rank && std::atoi(fail_rank) == rank) {
+        std::fprintf(stderr, "[rank %d] RTNW_DIST_FAIL_RANK: exiting before rt_dist_init\n", rank);
+        return 3;
+    }
     rt_scene_desc *desc = nullptr;   // the reference's builder, as a fresh process would run it
     if (rt_builtin_scene_desc(o.scene.c_str(), &desc) != RT_OK) { std::fprintf(stderr, "%s\n", rt_last_error()); return 2; }
     rt_scene *scene = nullptr;
@@ -127,12 +136,25 @@ int main(int argc, char **argv) {
     }
     close(fds[0]);
     close(fds[1]);
-    int worst = 0;
-    for (pid_t k : kids) {
+    // The first rank to fail stops the others: a peer of a rank that died before the
+    // communicator existed, or before the gather, would otherwise wait forever in
+    // ncclCommInitRank / ncclGather.  Returns the first failure's code.
+    int first = 0;
+    size_t left = kids.size();
+    while (left > 0) {
         int status = 0;
-        waitpid(k, &status, 0);
+        const pid_t k = waitpid(-1, &status, 0);
+        if (k < 0) break;
+        --left;
+        for (pid_t &kid : kids)
+            if (kid == k) kid = 0;
         const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + WTERMSIG(status);
-        if (code > worst) worst = code;
+        if (code != 0 && first == 0) {
+            first = code;
+            std::fprintf(stderr, "[launcher] a rank exited with %d: stopping the other ranks\n", code);
+            for (pid_t kid : kids)
+                if (kid > 0) kill(kid, SIGTERM);
+        }
     }
-    return worst;
+    return first;
 }

@@ -259,7 +259,11 @@ int64_t rt_rank_pixels(int nx, int ny, int rank, int world, int32_t *tiles, int6
 /* Scatters packed tiles (rt_render_tiles' output layout) into an nx x ny x 3 image. */
 int rt_unpack_tiles(const float *packed, const int32_t *tiles, int64_t ntiles, int nx, int ny, float *image);
 /* The whole rank job: this rank's pixels -> rt_render_tiles -> rt_dist_gather -> on the
- * root, the full nx x ny x 3 mean image in host memory (`image`; NULL on other ranks). */
+ * root, the full nx x ny x 3 mean image in host memory (`image`; NULL on other ranks).
+ * Mean images only: RT_FLAG_SUM_IN / RT_FLAG_SUM_OUT return RT_ERR_INVALID (on every
+ * rank alike).  A rank whose render fails still joins the gather; one that cannot
+ * allocate its buffers aborts the communicator (ncclCommAbort, later calls on it fail)
+ * and its launcher must stop the peers waiting in the gather. */
 int rt_dist_render(rt_dist *d, rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p, float *image,
                    rt_stats *stats);
 

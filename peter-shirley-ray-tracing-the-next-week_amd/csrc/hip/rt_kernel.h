@@ -82,3 +82,5 @@ extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int n
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);
 // Static LDS bytes of the LDS-BVH variant (its dynamic part: nodes + stacks).
 extern "C" int rt_megakernel_lds_static_bytes(void);
+// the largest static LDS (bytes) the compiler gave any LDS-BVH variant (hipFuncGetAttributes), 0 if unknown
+extern "C" int rt_megakernel_lds_static_actual(void);

@@ -29,6 +29,7 @@
 // Arithmetic follows the reference's float/double promotions; the file is compiled
 // with -ffp-contract=off so no FMA is introduced where the reference has none (the
 // BVH slab test, which decides nothing about the result, uses explicit fmaf).
+#include <algorithm>
 #include <type_traits>
 
 #include "rt_device.h"
@@ -551,13 +552,11 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
     size_t dyn = 0;
     if (kLds == 1) {
         dyn = RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES(a->stack_depth);
-        static bool attr = false;   // dynamic LDS above the default limit, once per variant
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               RT_LDS_BUDGET - rt_megakernel_lds_static_bytes());
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
+        // dynamic LDS above the default limit: the attribute is set on the current
+        // device's function before every launch (cheap, and right for any device and
+        // any thread, where a once-per-process flag is not)
+        hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(kLds == 1 ? RT_LDS_BLOCK : RT_BLOCK), dyn, stream, *a);
     return hipGetLastError();
@@ -614,6 +613,17 @@ extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int 
     if (width == 8) return occupancy_width<8, 0>(blocks_per_cu, mode);
     if (width == RT_BVH_CW8) return occupancy_width<RT_BVH_CW8, 0>(blocks_per_cu, mode);
     return width == 4 ? occupancy_width<4, 0>(blocks_per_cu, mode) : occupancy_width<2, 0>(blocks_per_cu, mode);
+}
+
+template <int kFeat>
+static int lds_static_of() {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, (const void *)rt_megakernel<false, false, 2, kFeat, 1>) != hipSuccess) return 0;
+    return (int)fa.sharedSizeBytes;
+}
+extern "C" int rt_megakernel_lds_static_actual(void) {
+    return std::max(std::max(lds_static_of<0>(), lds_static_of<RT_FEAT_INST>()),
+                    std::max(lds_static_of<RT_FEAT_CHECKER | RT_FEAT_PRESCAN>(), lds_static_of<RT_FEAT_ALL>()));
 }
 
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera

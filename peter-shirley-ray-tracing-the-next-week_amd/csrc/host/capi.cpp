@@ -545,8 +545,17 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
                           rt_megakernel_lds_static_bytes();
         bool want = true;
         if (const char *e = std::getenv("RTNW_LDS_BVH")) want = std::atoi(e) != 0;
+        // the budget is this device's LDS per CU (160 KiB on gfx950), and the static part
+        // the compiled variant's own (hipFuncGetAttributes) if larger than the estimate:
+        // a scene that does not fit keeps its nodes in HBM instead of failing to launch
+        int lds_cu = RT_LDS_BUDGET;
+        if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess ||
+            lds_cu <= 0)
+            lds_cu = 0;
+        const long stat = std::max<long>(rt_megakernel_lds_static_bytes(), rt_megakernel_lds_static_actual());
+        const long need_actual = need - rt_megakernel_lds_static_bytes() + stat;
         s->lds_nodes = want && !s->scan && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
-                       s->nnodes <= RT_LDS_NODE_CAP && need <= RT_LDS_BUDGET;
+                       s->nnodes <= RT_LDS_NODE_CAP && need_actual <= std::min<long>(RT_LDS_BUDGET, lds_cu);
         if (s->lds_nodes)
             for (int mode = 0; mode < 3; mode++) s->grid[mode] = s->cus;
     }
@@ -886,8 +895,16 @@ int rt_checkpoint_read(const char *path, rt_checkpoint *hdr, float *sums, uint64
     if (!f) return fail(RT_ERR_INVALID, std::string("cannot open ") + path);
     rt_checkpoint h;
     int rc = RT_OK;
+    // the file's own size bounds `count` before anyone sizes a buffer by it: header +
+    // count floats + the 8-byte checksum, and count = 3 x (pixels of a job <= nx x ny)
+    long fsize = -1;
+    if (std::fseek(f, 0, SEEK_END) == 0) fsize = std::ftell(f);
+    std::rewind(f);
     if (std::fread(&h, sizeof h, 1, f) != 1 || h.magic != RT_CHECKPOINT_MAGIC || h.version != RT_CHECKPOINT_VERSION) {
         rc = fail(RT_ERR_INVALID, std::string("not a checkpoint: ") + path);
+    } else if (h.nx <= 0 || h.ny <= 0 || h.count % 3 != 0 || h.count > 3ull * (uint64_t)h.nx * (uint64_t)h.ny ||
+               fsize < 0 || (uint64_t)fsize != sizeof h + h.count * sizeof(float) + sizeof(uint64_t)) {
+        rc = fail(RT_ERR_INVALID, std::string("corrupt checkpoint header (count / image size / file size): ") + path);
     } else if (sums) {   // sums == NULL: header only (to size the buffer)
         if (h.count > cap) {
             rc = fail(RT_ERR_INVALID, "checkpoint larger than the buffer");

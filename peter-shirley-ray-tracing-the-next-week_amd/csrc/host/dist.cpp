@@ -40,6 +40,7 @@ static_assert(sizeof(ncclUniqueId) == RT_DIST_ID_BYTES, "ncclUniqueId size");
 struct rt_dist {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1, device = 0;
+    bool aborted = false;   // ncclCommAbort after a local failure (rt_dist_render)
 };
 
 extern "C" {
@@ -73,13 +74,14 @@ int rt_dist_init(const uint8_t *id, int rank, int world, int device, rt_dist **o
 
 void rt_dist_destroy(rt_dist *d) {
     if (!d) return;
-    if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->comm && !d->aborted) (void)ncclCommDestroy(d->comm);
     delete d;
 }
 
 int rt_dist_gather(rt_dist *d, const float *send_dev, uint64_t count, float *recv_dev, int root, void *stream) {
     if (!d || !send_dev || root < 0 || root >= d->world || (d->rank == root && !recv_dev))
         return fail(RT_ERR_INVALID, "rt_dist_gather: bad argument");
+    if (d->aborted) return fail(RT_ERR_HIP, "rt_dist_gather: the communicator was aborted after an earlier failure");
     HIP_TRY(hipSetDevice(d->device));
     NCCL_TRY(ncclGather(send_dev, recv_dev, (size_t)count, ncclFloat32, root, d->comm, (hipStream_t)stream));
     return RT_OK;
@@ -135,9 +137,18 @@ int rt_unpack_tiles(const float *packed, const int32_t *tiles, int64_t ntiles, i
 
 int rt_dist_render(rt_dist *d, rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p, float *image,
                    rt_stats *stats) {
+    // Argument errors below depend only on (nx, ny, world, flags), which every rank of
+    // one job passes alike: all ranks return them before the gather, none is left
+    // waiting in the collective.
     if (!d || !s || !cam || !p) return fail(RT_ERR_INVALID, "rt_dist_render: bad argument");
+    if (d->aborted) return fail(RT_ERR_HIP, "rt_dist_render: the communicator was aborted after an earlier failure");
+    // The shares are rendered into freshly zeroed buffers and gathered as means:
+    // running sums in (RT_FLAG_SUM_IN) would start from zero but still be scaled by
+    // 1/(sample_offset + spp), and sums out (RT_FLAG_SUM_OUT) would reach the root
+    // labelled as a mean image.  Progressive multi-GPU renders use rt_render_tiles.
+    if (p->flags & (RT_FLAG_SUM_IN | RT_FLAG_SUM_OUT))
+        return fail(RT_ERR_INVALID, "rt_dist_render: RT_FLAG_SUM_IN / RT_FLAG_SUM_OUT are not supported (mean images only)");
     if (d->rank == 0 && !image) return fail(RT_ERR_INVALID, "rt_dist_render: the root needs an image buffer");
-    HIP_TRY(hipSetDevice(d->device));
     // every rank's pixel count, so that the gather's per-rank count (the largest) is agreed
     int64_t nmax = 0;
     for (int r = 0; r < d->world; ++r) {
@@ -160,11 +171,19 @@ int rt_dist_render(rt_dist *d, rt_scene *s, const rt_camera_desc *cam, const rt_
         if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
         return rc == RT_OK;
     };
-    if (!hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate") ||
+    // A local resource failure (device, stream, buffers) cannot join the gather: the
+    // communicator is aborted (ncclCommAbort) so that this rank does not leave a
+    // half-open collective behind, and the error returned; the peers then block in
+    // their gather until the job's launcher stops them (examples/render_dist.cpp and
+    // bench.py's launch_ranks stop every rank once one exits with an error).
+    if (!hip_ok(hipSetDevice(d->device), "hipSetDevice") ||
+        !hip_ok(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate") ||
         !hip_ok(hipMalloc(&send, count * sizeof(float)), "hipMalloc send") ||
         !hip_ok(hipMemsetAsync(send, 0, count * sizeof(float), stream), "hipMemset") ||
         (d->rank == 0 && !hip_ok(hipMalloc(&recv, count * d->world * sizeof(float)), "hipMalloc recv"))) {
         cleanup();
+        (void)ncclCommAbort(d->comm);
+        d->aborted = true;
         return rc;
     }
     // A rank whose render fails still joins the gather (with its zeroed buffer), so the

@@ -178,3 +178,20 @@ def test_rccl_one_rank_communicator_gather_equals_render_tile():
     torch.cuda.synchronize()
     assert torch.equal(recv, data)
     d.close()
+
+
+@pytest.mark.gpu
+def test_dist_render_refuses_running_sum_flags():
+    """rt_dist_render gathers freshly rendered MEAN shares: RT_FLAG_SUM_IN (which would
+    start from zero sums yet divide by sample_offset + spp) and RT_FLAG_SUM_OUT (sums
+    delivered as the root's mean image) are refused, on every rank alike."""
+    sc = rtnw.Scene.builtin("final", device=0)
+    cam = rtnw.Camera.preset("cornell", 16, 16)
+    d = rtnw.Dist(rtnw.dist_unique_id(), 0, 1, 0)
+    for flag in (rtnw.RT_FLAG_SUM_IN, rtnw.RT_FLAG_SUM_OUT):
+        with pytest.raises(rtnw.RtError, match="not supported"):
+            d.render(sc, cam, rtnw.RenderParams(16, 16, 2, seed=1, flags=flag, sample_offset=3))
+    img, st = d.render(sc, cam, rtnw.RenderParams(16, 16, 2, seed=1))   # the communicator is still usable
+    assert st["samples"] == 16 * 16 * 2 and np.isfinite(img).all()
+    d.close()
+    sc.close()

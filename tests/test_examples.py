@@ -61,3 +61,26 @@ def test_dist_example_one_rank_matches_python_path():
     sc = rtnw.Scene.builtin("final")
     mean = sc.render_tile(rtnw.Camera.preset("cornell", 40, 32), rtnw.RenderParams(40, 32, 8, seed=5), 0, 0, 40, 32)
     assert open(out, "rb").read() == rtnw.ppm_text(rtnw.quantize(mean))
+
+
+def _run_dist_with_failing_rank():
+    _build()
+    env = dict(os.environ, RTNW_DIST_FAIL_RANK="1")
+    return subprocess.run([os.path.join(EX, "render_dist"), "--ranks", "2", "--nx", "16", "--ny", "16", "--ns", "1",
+                           "--ppm", os.devnull], capture_output=True, text=True, timeout=120, env=env)
+
+
+@pytest.mark.skipif(rtnw.device_count() > 0, reason="a GPU is present")
+def test_dist_example_with_a_failing_rank_ends_without_gpu():
+    r = _run_dist_with_failing_rank()
+    assert r.returncode != 0
+
+
+@pytest.mark.gpu
+def test_dist_example_stops_the_ranks_when_one_fails():
+    """Rank 1 exits after the communicator id exchange, before ncclCommInitRank (as a
+    failed scene build would): rank 0 would wait in ncclCommInitRank forever; the
+    launcher stops it and returns rank 1's code."""
+    r = _run_dist_with_failing_rank()
+    assert r.returncode == 3, r.stderr[-2000:]
+    assert "stopping the other ranks" in r.stderr

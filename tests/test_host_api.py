@@ -231,6 +231,16 @@ def test_checkpoint_round_trip_and_corruption(tmp_path):
         rtnw.read_checkpoint(str(tmp_path / "c.rtck"))
     with pytest.raises(rtnw.RtError):
         rtnw.read_checkpoint(str(tmp_path / "missing.rtck"))
+    # a crafted header is refused before any buffer is sized by it: count beyond the
+    # image (3 nx ny), count not matching the file size, a non-positive image
+    off = rtnw.RtCheckpoint.count.offset
+    for field_off, value, width in ((off, 1 << 40, 8), (off, 3 * 20 * 10 - 3, 8),
+                                    (rtnw.RtCheckpoint.nx.offset, 0, 4)):
+        raw = bytearray(path.read_bytes())
+        raw[field_off:field_off + width] = int(value).to_bytes(width, "little")
+        (tmp_path / "d.rtck").write_bytes(bytes(raw))
+        with pytest.raises(rtnw.RtError, match="corrupt checkpoint header"):
+            rtnw.read_checkpoint(str(tmp_path / "d.rtck"))
 
 
 def test_shared_reciprocal_division_is_ieee(tmp_path):

@@ -63,6 +63,14 @@ for step in "$@"; do
             run pmc_l1 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/pmc_l1 -o run --output-format csv -- $B ;;
     dist2n) run dist2n 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --dist-backend gloo --spp 64 --steps 2 --warmup 1 --ppm gpurun_out/dist2n.ppm ;;
     c5one)  run c5one 600 python3 bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline --ppm gpurun_out/c5one.ppm ;;
+    lanes)  export TMPDIR=/tmp   # VALU lane utilisation of the timed kernel, per config (LANES_CFGS)
+            for c in ${LANES_CFGS:-c4 c2 c3}; do
+              run lanes_$c 300 timeout -s KILL 240 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/lanes_$c -o run --output-format csv -- python3 bench.py --config $c --steps 1 --warmup 0 --no-cpu-baseline
+            done
+            run lanes_sum 60 python3 tools/lanes_summary.py gpurun_out gpurun_out/lanes.json ;;
+    dist2s) run dist2s 600 python3 bench.py --gpus 2 --dist-backend gloo --spp 64 --steps 2 --warmup 1 --no-cpu-baseline --dump gpurun_out/dist2s.npy ;;
+    probe)  run probe 600 python3 tools/scaling_probe.py --out gpurun_out/scaling_probe.json ;;
+    c5)     run c5 600 python3 bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmcsum) run pmcsum 60 python3 tools/pmc_traffic.py gpurun_out gpurun_out/profile_summary 250000000 c4 ;;
     ab)     run ab 1200 python3 tools/ab.py $AB_LIBS --rounds ${AB_ROUNDS:-2} ;;
     *) echo "unknown step $step"; exit 2 ;;

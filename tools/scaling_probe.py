@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
 """tools/scaling_probe.py — the multi-GPU bench's per-rank work, measured on ONE GPU.
 
-For each N in --ranks, builds the image bench.py uses at N GPUs and the tile lists
-rank_layout deals to the N ranks, then renders every rank's tile list on this GPU
-one after the other (HIP-event kernel time each).  Reports, per N:
-  * per-sample cost of the N-GPU image relative to the 1-GPU image (weak scaling
-    holds per-GPU work fixed only if this stays ~1), and
-  * max/mean of the per-rank kernel times (load imbalance: the bench's value is set
-    by the slowest rank).
-Diagnostic only; the 8-GPU run itself is the driver's."""
+`bench.py --gpus N` renders config 5 (final() 1000 x 1000 x 1000 spp, strong
+scaling) as N interleaved pixel shares (rtnw.pixels_for_rank: rank (ry, rx) of
+a x b renders x = rx mod a, y = ry mod b), one per GPU, then one gather.  For each N
+this renders every share of that job on this GPU, one after the other (median
+HIP-event kernel time of --repeats launches each), and reports per N:
+  * rank_ms and imbalance = max/mean (the N-GPU step is set by the slowest rank);
+  * ns_per_sample of the shares against the whole image on one GPU (an interleaved
+    share is a sub-sampled view: its wave claims span a x b times the pixels);
+  * predicted_msamples_per_s = the job's samples / the slowest share's time, i.e.
+    the N-GPU value if the gather (12 MB) and the rendezvous cost nothing.
+Diagnostic only; the 8-GPU run itself is the driver's.
+
+    python tools/scaling_probe.py [--ranks 1,2,4,8] [--spp 1000] [--repeats 3] [--out probe.json]
+"""
 import argparse
 import json
 import os
@@ -17,68 +23,56 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "peter-shirley-ray-tracing-the-next-week_amd"))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
 import rtnw  # noqa: E402
 
-def wide_image(n):
-    w, h, k = 500, 500, 1
-    while k < n:
-        w, h, k = (w * 2, h, k * 2) if w <= h else (w, h * 2, k * 2)
-    return w, h
 
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c5", choices=sorted(bench.CONFIGS))
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--spp", type=int, default=0, help="default: the config's (c5: 1000)")
+    ap.add_argument("--repeats", type=int, default=3, help="median of this many launches per share")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--ranks", default="1,2,4,8")
-ap.add_argument("--spp", type=int, default=256)
-ap.add_argument("--tile", type=int, default=bench.TILE)
-ap.add_argument("--wide", action="store_true", help="the earlier N-GPU images: 500x500, 1000x500, 1000x1000, 2000x1000")
-ap.add_argument("--order", default=bench.LAYOUT, choices=["diagonal", "hashed", "interleaved"])
-ap.add_argument("--reverse", action="store_true", help="render the ranks last to first")
-ap.add_argument("--repeats", type=int, default=3, help="median of this many launches per rank")
-ap.add_argument("--fullres", action="store_true",
-                help="instead: whole images of side 500 sqrt(N) and 2:1 ones at spp / N (equal sample counts)")
-args = ap.parse_args()
-
-dev = torch.device("cuda", 0)
-scene = rtnw.Scene.builtin("final", device=0)
-if args.fullres:
+    scene_name, nx, ny, spp, _ = bench.CONFIGS[args.config]
+    spp = args.spp or spp
+    cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
     dev = torch.device("cuda", 0)
-    scene = rtnw.Scene.builtin("final", device=0)
-    for n in [int(x) for x in args.ranks.split(",")]:
-        for nx, ny in ({bench.image_for(n), wide_image(n)}):
-            spp = args.spp // n
-            cam = rtnw.Camera.preset("cornell", nx, ny)
-            params = rtnw.RenderParams(nx, ny, spp, max_depth=50, seed=2024)
-            out = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
-            stream = torch.cuda.current_stream(dev).cuda_stream
-            t = sorted(scene.render_tiles(cam, params, [(0, 0, nx, ny)], out.data_ptr(), stream)["kernel_ms"]
-                       for _ in range(args.repeats + 1))[: args.repeats]
-            print(json.dumps({"image": [nx, ny], "spp": spp, "ns_per_sample": t[len(t) // 2] * 1e6 / (nx * ny * spp)}),
-                  flush=True)
-    sys.exit(0)
-res = {"spp": args.spp, "tile": args.tile, "order": args.order, "wide": args.wide, "runs": []}
-base = None
-for n in [int(x) for x in args.ranks.split(",")]:
-    nx, ny = wide_image(n) if args.wide else bench.image_for(n)
-    cam = rtnw.Camera.preset("cornell", nx, ny)
-    params = rtnw.RenderParams(nx, ny, args.spp, max_depth=50, seed=2024)
-    tiles, counts = rtnw.rank_layout(nx, ny, args.tile, n, args.order) if n > 1 else ([[(0, 0, nx, ny)]], [nx * ny * 3])
-    out = torch.zeros(max(counts), dtype=torch.float32, device=dev)
+    scene = rtnw.Scene.builtin(scene_name, device=0)
+    cam = rtnw.Camera.preset(cam_name, nx, ny)
+    params = rtnw.RenderParams(nx, ny, spp, max_depth=depth, background=bg, seed=2024)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    scene.render_tiles(cam, params, tiles[0], out.data_ptr(), stream, stats=True)   # warm
-    ms = [0.0] * n
-    for r in (reversed(range(n)) if args.reverse else range(n)):
-        t = sorted(scene.render_tiles(cam, params, tiles[r], out.data_ptr(), stream, stats=True)["kernel_ms"]
-                   for _ in range(args.repeats))
-        ms[r] = t[len(t) // 2]
-    ns_per_sample = sum(ms) * 1e6 / (nx * ny * args.spp)
-    if base is None:
-        base = ns_per_sample
-    row = {"n": n, "image": [nx, ny], "rank_ms": ms, "ns_per_sample": ns_per_sample,
-           "cost_vs_1gpu_image": ns_per_sample / base, "imbalance_max_over_mean": max(ms) / (sum(ms) / n)}
-    res["runs"].append(row)
-    print(json.dumps(row), flush=True)
-scene.close()
-print(json.dumps(res))
+    out = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
+    res = {"config": args.config, "image": [nx, ny], "spp": spp, "layout": bench.LAYOUT, "runs": []}
+    base = None
+    for n in [int(x) for x in args.ranks.split(",")]:
+        shares = [rtnw.pixels_for_rank(nx, ny, r, n) for r in range(n)] if n > 1 else [[(0, 0, nx, ny)]]
+        scene.render_tiles(cam, params, shares[0], out.data_ptr(), stream)   # warm
+        ms, batches = [], []
+        for r in range(n):
+            runs = [scene.render_tiles(cam, params, shares[r], out.data_ptr(), stream) for _ in range(args.repeats)]
+            ms.append(float(np.median([s["kernel_ms"] for s in runs])))
+            batches.append(int(runs[0]["batches"]))
+        ns = sum(ms) * 1e6 / (nx * ny * spp)
+        base = base or ns
+        row = {"n": n, "interleave": list(rtnw.interleave_factors(n)), "rank_ms": ms, "batches": batches,
+               "max_ms": max(ms), "mean_ms": sum(ms) / n, "imbalance_max_over_mean": max(ms) / (sum(ms) / n),
+               "ns_per_sample": ns, "cost_vs_1gpu_image": ns / base,
+               "predicted_msamples_per_s": nx * ny * spp / (max(ms) / 1e3) / 1e6,
+               "predicted_strong_scaling_efficiency": base * nx * ny * spp / 1e6 / (n * max(ms))}
+        res["runs"].append(row)
+        print(json.dumps(row), flush=True)
+    scene.close()
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
