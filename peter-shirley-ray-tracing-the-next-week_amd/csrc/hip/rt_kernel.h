@@ -63,7 +63,9 @@ struct RtKernelArgs {
     const uint32_t *job_xy;   // x | y << 16 per job pixel (image coords)
     uint32_t npix;
     uint32_t nitems;          // npix * nchunks
-    uint32_t claim;           // work items per wave-level claim (a multiple of 64)
+    uint32_t claim;           // work items per wave-level claim (a multiple of 64) ...
+    uint32_t nbig;            // ... for the first nbig claims; the rest (the launch's tail) claim
+    uint32_t claim_tail;      //     claim_tail items each, so that waves run dry together
     float4 *slab;             // [nchunks][npix] partial sums of this launch's sample batch
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)

@@ -53,6 +53,11 @@ namespace {
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
+// Wave priority (s_setprio) once a wave finds the work pool empty (0: unchanged).
+#ifndef RT_EXHAUST_PRIO
+#define RT_EXHAUST_PRIO 0
+#endif
+
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -156,6 +161,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     Counters cnt;
     uint64_t prof[4] = {0, 0, 0, 0};
     uint64_t stamp = kProf ? __builtin_amdgcn_s_memtime() : 0;
+    // wave timeline (kProf): start, first sight of the empty pool, end (s_memrealtime: one clock for all CUs)
+    const uint64_t rt_start = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t rt_exhaust = 0;
     auto mark = [&](int k) {
         if (kProf) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -183,12 +191,28 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // regeneration.  They wait in the wave's LDS slots until a lane takes one.
     auto refill = [&]() {   // all 64 lanes; wave-uniform outcome
         if (pool_next == pool_end) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(A.counter, A.claim);
-            base = __shfl(base, 0);
-            if (base >= A.nitems) { exhausted = true; return; }
+            // claims are counted, not items: claim k < nbig covers A.claim items, later
+            // ones A.claim_tail (the launch's last items go out in small claims, so that
+            // no wave is left with a large claim while the others have run dry)
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(A.counter, 1u);
+            k = __shfl(k, 0);
+            const uint32_t big = min(k, A.nbig);
+            const uint64_t b64 = (uint64_t)big * A.claim + (uint64_t)(k - big) * A.claim_tail;
+            const uint32_t base = (uint32_t)min(b64, (uint64_t)A.nitems);
+            const uint32_t size = k < A.nbig ? A.claim : A.claim_tail;
+            if (base >= A.nitems) {
+                exhausted = true;
+                if (kProf) rt_exhaust = __builtin_amdgcn_s_memrealtime();
+#if RT_EXHAUST_PRIO
+                // the launch's end: a wave whose pool ran dry finishes its last paths at
+                // raised priority, ahead of the waves still busy with their claims
+                __builtin_amdgcn_s_setprio(RT_EXHAUST_PRIO);
+#endif
+                return;
+            }
             pool_next = base;
-            pool_end = min(base + A.claim, A.nitems);
+            pool_end = min(base + size, A.nitems);
         }
         const uint32_t n = min(64u, pool_end - pool_next);
         if (lane < n) {
@@ -488,8 +512,19 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
 #endif
     }
-    if (kProf && lane == 0)
+    if (kProf && lane == 0) {
         for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_CNT_N + k], (unsigned long long)prof[k]);
+        // minima as maxima of the complement (the slots start at 0)
+        const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+        unsigned long long *T = A.stats + RT_CNT_N + 9;
+        atomicMax(&T[0], ~(unsigned long long)rt_start);
+        atomicMax(&T[1], ~(unsigned long long)(rt_exhaust ? rt_exhaust : rt_end));
+        atomicMax(&T[2], (unsigned long long)(rt_exhaust ? rt_exhaust : rt_end));
+        atomicMax(&T[3], ~rt_end);
+        atomicMax(&T[4], rt_end);
+        atomicAdd(&T[5], rt_end - (unsigned long long)rt_start);
+        atomicAdd(&T[6], 1ull);
+    }
     if (kCount) {
         uint64_t w[5] = {cnt.w_iters, cnt.w_nodes, cnt.w_prims, cnt.w_rius, cnt.l_rius};
         for (int k = 0; k < 5; ++k) {

@@ -574,6 +574,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     return RT_OK;
 }
 
+// Small claims per wave at the end of a launch (render_tiles' claim sizes).
+#ifndef RT_TAIL_CLAIMS
+#define RT_TAIL_CLAIMS 32
+#endif
+
 // Partial-sum slab budget per launch (bytes; env RTNW_SLAB_BUDGET overrides, for tests).
 // A job whose slab would be larger runs as several launches over sample batches.
 #ifndef RT_SLAB_BUDGET
@@ -743,10 +748,19 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         // Claim size: up to 512 items per atomic (64 -> 512 is 81.6 -> 76.9 ms on c4:
         // fewer round trips to the one contended counter), at least 8
         // claims per wave so that small jobs still spread over every wave.
+        // The last RT_TAIL_CLAIMS claims per wave are of 64 items: with 512-item claims
+        // to the end, the waves ran dry over 2.4 ms (the first found the pool empty at
+        // 54.1 ms of a 57.1-ms launch, the last at 56.5; with 64-item claims over 0.5 ms,
+        // but every claim is a round trip to the one device-scope counter:
+        // tools/tail_probe.py).
         {
             uint64_t c = std::min<uint64_t>(std::max<uint64_t>(nitems / (waves * 8) / 64 * 64, 64), 512);
+            uint64_t tail = 64 * RT_TAIL_CLAIMS * waves;
             if (const char *e = std::getenv("RTNW_CLAIM")) c = (uint64_t)std::max(1, std::atoi(e)) * 64;   // x 64 items
+            if (const char *e = std::getenv("RTNW_TAIL_CLAIMS")) tail = 64 * (uint64_t)std::max(0, std::atoi(e)) * waves;
             a.claim = (uint32_t)c;
+            a.claim_tail = 64;
+            a.nbig = (uint32_t)(nitems > tail ? (nitems - tail) / c : 0);
         }
         const int rmode = (b == 0 ? RT_RESOLVE_FIRST : 0) | (b + 1 == nbatches ? RT_RESOLVE_LAST : 0) |
                           (sum_in ? RT_RESOLVE_SUM_IN : 0) | (sum_out ? RT_RESOLVE_RAW : 0);
@@ -797,12 +811,20 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->lane_sphere_draw_trips = (double)w[4];
         }
         if (prof) {
-            unsigned long long c[RT_CNT_N + 4];
+            unsigned long long c[RT_CNT_N + 16];
             HIP_TRY(hipMemcpy(c, s->stats, sizeof c, hipMemcpyDeviceToHost));
             stats->cycles_claim = (double)c[RT_CNT_N + 0];
             stats->cycles_traverse = (double)c[RT_CNT_N + 1];
             stats->cycles_media = (double)c[RT_CNT_N + 2];
             stats->cycles_shade = (double)c[RT_CNT_N + 3];
+            // wave timeline of the last batch, s_memrealtime at 100 MHz (kernel: kProf)
+            const unsigned long long *T = c + RT_CNT_N + 9;
+            const double t0 = (double)~T[0], us = 0.01;
+            stats->wave_exhaust_first_us = ((double)~T[1] - t0) * us;
+            stats->wave_exhaust_last_us = ((double)T[2] - t0) * us;
+            stats->wave_end_first_us = ((double)~T[3] - t0) * us;
+            stats->wave_end_last_us = ((double)T[4] - t0) * us;
+            stats->wave_end_mean_us = T[6] ? (double)T[5] / (double)T[6] * us : 0.0;
         }
         stats->grid = (double)s->grid[mode];
         stats->lds_level = s->lds_nodes ? 1.0 : 0.0;

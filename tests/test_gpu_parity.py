@@ -354,12 +354,14 @@ def test_baseline_configs_at_full_spp_against_oracle_crops(scene, nx, ny, ns):
     assert min(exact) > 0.5, exact
 
 
-@pytest.mark.parametrize("claim", ["1", "3", "16"])
-def test_claim_size_does_not_change_the_image(monkeypatch, claim):
-    """Work items per wave-level claim (RTNW_CLAIM x 64) only change which lane runs
-    which sample: the partial-sum slot of a sample is fixed, so images agree bitwise."""
+@pytest.mark.parametrize("claim,tail", [("1", "0"), ("3", "2"), ("16", "0"), ("16", "1"), ("8", "50")])
+def test_claim_size_does_not_change_the_image(monkeypatch, claim, tail):
+    """Work items per wave-level claim (RTNW_CLAIM x 64) and the small claims at the
+    launch's end (RTNW_TAIL_CLAIMS per wave) only change which lane runs which sample:
+    the partial-sum slot of a sample is fixed, so images agree bitwise."""
     ref = gpu_render("final", 64, 40, 8, seed=8, chunk=1)
     monkeypatch.setenv("RTNW_CLAIM", claim)
+    monkeypatch.setenv("RTNW_TAIL_CLAIMS", tail)
     img = gpu_render("final", 64, 40, 8, seed=8, chunk=1)
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
 
