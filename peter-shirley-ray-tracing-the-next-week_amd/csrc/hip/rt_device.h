@@ -1005,13 +1005,15 @@ __device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec
 // pushed the kernel past the SGPR limit and came back as per-iteration v_readlanes.
 typedef float CamV4 __attribute__((ext_vector_type(4)));
 struct CamView { V3 llc, hor, ver, org, cu, cv; float t0, t1, lens; };
+// Written float by float: whole-vector initialisers from the kernel-argument arrays
+// made the compiler assemble them in scratch memory.
 __device__ __forceinline__ void store_camera(const RtKernelArgs &A, CamV4 *lds) {
-    lds[0] = CamV4{A.llc[0], A.llc[1], A.llc[2], A.ct0};
-    lds[1] = CamV4{A.hor[0], A.hor[1], A.hor[2], A.ct1};
-    lds[2] = CamV4{A.ver[0], A.ver[1], A.ver[2], A.lens};
-    lds[3] = CamV4{A.org[0], A.org[1], A.org[2], 0.f};
-    lds[4] = CamV4{A.cu[0], A.cu[1], A.cu[2], 0.f};
-    lds[5] = CamV4{A.cv[0], A.cv[1], A.cv[2], 0.f};
+    float *f = reinterpret_cast<float *>(lds);
+    const float v[24] = {A.llc[0], A.llc[1], A.llc[2], A.ct0,  A.hor[0], A.hor[1], A.hor[2], A.ct1,
+                         A.ver[0], A.ver[1], A.ver[2], A.lens, A.org[0], A.org[1], A.org[2], 0.f,
+                         A.cu[0],  A.cu[1],  A.cu[2],  0.f,    A.cv[0],  A.cv[1],  A.cv[2],  0.f};
+#pragma unroll
+    for (int k = 0; k < 24; ++k) f[k] = v[k];
 }
 typedef __attribute__((address_space(3))) const volatile CamV4 LdsCamV4;   // keeps ds_read (not flat)
 __device__ __forceinline__ CamView load_camera(const CamV4 *lds) {
@@ -1086,12 +1088,11 @@ struct MediumRec {
 template <int kBlock>
 __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds) {
     const int n = min(A.nmedia, RT_LDS_MEDIA);
-    for (int i = threadIdx.x; i < n; i += kBlock) {
-        MediumRec m;
-        m.md = A.media[i];
-        m.g0 = A.bprims[m.md.x * 4 + 0];
-        m.mm = A.bprims[m.md.x * 4 + 1];
-        lds[i] = m;
+    for (int i = threadIdx.x; i < n; i += kBlock) {   // field by field: a whole-struct copy went through scratch
+        const int4 md = A.media[i];
+        lds[i].md = md;
+        lds[i].g0 = A.bprims[md.x * 4 + 0];
+        lds[i].mm = A.bprims[md.x * 4 + 1];
     }
 }
 

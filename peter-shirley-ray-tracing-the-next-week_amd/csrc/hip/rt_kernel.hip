@@ -53,11 +53,6 @@ namespace {
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
-// Wave priority (s_setprio) once a wave finds the work pool empty (0: unchanged).
-#ifndef RT_EXHAUST_PRIO
-#define RT_EXHAUST_PRIO 0
-#endif
-
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -92,12 +87,14 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
+    // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(lds_dyn + 4 * RT_LDS_NODE_CAP) +
-                               (threadIdx.x >> 6) * (uint32_t)A.stack_depth * 64u + lane
-                         : &lds_stack[kMode ? 0 : threadIdx.x >> 6][0][lane];
-    CoopSlot *slots = lds_slots[threadIdx.x >> 6];
-    uint64_t *pre_key = lds_pre_key[threadIdx.x >> 6];
-    float2 *pre_uv = lds_pre_uv[threadIdx.x >> 6];
+                               wave * (uint32_t)A.stack_depth * 64u + lane
+                         : &lds_stack[kMode ? 0 : wave][0][lane];
+    CoopSlot *slots = lds_slots[wave];
+    uint64_t *pre_key = lds_pre_key[wave];
+    float2 *pre_uv = lds_pre_uv[wave];
     // the media records are read from LDS (one broadcast read per medium)
     load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) store_camera(A, lds_cam);
@@ -204,11 +201,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             if (base >= A.nitems) {
                 exhausted = true;
                 if (kProf) rt_exhaust = __builtin_amdgcn_s_memrealtime();
-#if RT_EXHAUST_PRIO
-                // the launch's end: a wave whose pool ran dry finishes its last paths at
-                // raised priority, ahead of the waves still busy with their claims
-                __builtin_amdgcn_s_setprio(RT_EXHAUST_PRIO);
-#endif
                 return;
             }
             pool_next = base;
