@@ -41,7 +41,7 @@
 static unsigned short g_canon_state[3] = {0, 0, 0};
 static int g_mode = 0;            // 0 canonical, 1 counter
 static uint64_t g_key = 0;        // counter mode: per-sample stream key
-static uint64_t g_draw = 0;       // counter mode: draws taken from the sample stream
+static uint64_t g_x = 0;          // counter mode: the sample's drand48 state (restarted at key mod 2^48)
 static int g_med_ctx = -1;        // >=0 while a constant_medium (ordinal k) is being hit
 static int g_bounce = 0;          // top-level world->hit calls in this sample
 
@@ -63,8 +63,9 @@ extern "C" double drand48(void) noexcept {
         uint64_t m = ((uint64_t)g_bounce << 8) | (uint64_t)g_med_ctx;
         return u48(mix64(mk + (m + 1) * kGamma));
     }
-    g_draw++;
-    return u48(mix64(g_key + g_draw * kGamma));
+    // drand48's own step on the sample's state (x = a x + c mod 2^48, x / 2^48)
+    g_x = (0x5DEECE66Dull * g_x + 0xBull) & 0xFFFFFFFFFFFFull;
+    return (double)g_x * 0x1p-48;
 }
 
 // -------------------------------------------------------- instrumentation nodes
@@ -422,7 +423,7 @@ int main(int argc, char **argv) {
         for (int i = 0; i < nx; i++) {
             vec3 col(0, 0, 0);
             for (int s = 0; s < ns; s++) {
-                if (g_mode == 1) { g_key = sample_key(seed, (uint32_t)(j * nx + i), (uint32_t)s); g_draw = 0; g_bounce = 0; }
+                if (g_mode == 1) { g_key = sample_key(seed, (uint32_t)(j * nx + i), (uint32_t)s); g_x = g_key & 0xFFFFFFFFFFFFull; g_bounce = 0; }
                 float u = float(i + drand48()) / float(nx);
                 float v = float(j + drand48()) / float(ny);
                 ray r = cam.get_ray(u, v);

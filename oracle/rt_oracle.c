@@ -71,17 +71,21 @@ static inline double u48(uint64_t z) { return (double)(z >> 16) * 0x1p-48; }
 typedef struct {
     int counter;
     uint64_t x;      /* canonical LCG state */
-    uint64_t key;    /* counter: sample key */
-    uint64_t n;      /* counter: draws taken */
+    uint64_t key;    /* counter: sample key (the medium stream's seed) */
+    uint64_t n;      /* unused */
 } rng_t;
 
+/* drand48's step (x = a x + c mod 2^48, draw = x / 2^48) in both modes: canonical is
+ * one stream for the whole run; counter restarts it per sample at x = key mod 2^48
+ * (rng_seed_sample), so a sample's draws do not depend on which other samples ran. */
 static inline double rng_next(rng_t *g) {
-    if (!g->counter) {
-        g->x = (LCG_A * g->x + LCG_C) & LCG_M;
-        return (double)g->x * 0x1p-48;
-    }
-    g->n++;
-    return u48(mix64(g->key + g->n * kGamma));
+    g->x = (LCG_A * g->x + LCG_C) & LCG_M;
+    return (double)g->x * 0x1p-48;
+}
+static inline void rng_seed_sample(rng_t *g, uint64_t key) {
+    g->key = key;
+    g->x = key & LCG_M;
+    g->n = 0;
 }
 static inline double rng_medium(rng_t *g, int bounce, int k) {
     if (!g->counter) return rng_next(g);
@@ -842,7 +846,7 @@ static v3 render_pixel(run_t *rn, const cam_t *cam, int i, int j, rng_t *g) {
     int chunk = p->chunk > 0 ? p->chunk : p->ns;
     v3 col = V(0, 0, 0), part = V(0, 0, 0);
     for (int s = 0; s < p->ns; s++) {
-        if (g->counter) { g->key = sample_key(p->seed, (uint32_t)(j * p->nx + i), (uint32_t)s + p->sample_offset); g->n = 0; }
+        if (g->counter) rng_seed_sample(g, sample_key(p->seed, (uint32_t)(j * p->nx + i), (uint32_t)s + p->sample_offset));
         float u = (float)(i + rng_next(g)) / (float)p->nx;                /* main.cpp:305-306 */
         float v = (float)(j + rng_next(g)) / (float)p->ny;
         ray_t r = camera_get_ray(cam, u, v, g);
@@ -945,12 +949,12 @@ void oracle_drand48(uint64_t x0, int n, double *out) {
 }
 
 void oracle_counter_draws(uint64_t seed, uint32_t pixel, uint32_t sample, int n, double *out) {
-    rng_t g; memset(&g, 0, sizeof g); g.counter = 1; g.key = sample_key(seed, pixel, sample);
+    rng_t g; memset(&g, 0, sizeof g); g.counter = 1; rng_seed_sample(&g, sample_key(seed, pixel, sample));
     for (int i = 0; i < n; i++) out[i] = rng_next(&g);
 }
 
 double oracle_medium_draw(uint64_t seed, uint32_t pixel, uint32_t sample, int bounce, int medium) {
-    rng_t g; memset(&g, 0, sizeof g); g.counter = 1; g.key = sample_key(seed, pixel, sample);
+    rng_t g; memset(&g, 0, sizeof g); g.counter = 1; rng_seed_sample(&g, sample_key(seed, pixel, sample));
     return rng_medium(&g, bounce, medium);
 }
 

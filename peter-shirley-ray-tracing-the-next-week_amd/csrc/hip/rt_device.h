@@ -68,22 +68,19 @@ __device__ __forceinline__ float div_by(float x, const Recip &r) { return r.ok ?
 __device__ __forceinline__ V3 at(const Ray &r, float t) { return add(r.o, scale(t, r.d)); }
 
 // ------------------------------------------------------------------- RNG
-// Counter streams: sample (pixel, s) draws u48(mix64(key + n*GAMMA)),
-// n = 1, 2, ...; constant_medium k at bounce b draws from a second keyed stream.
+// Per-sample drand48 streams: sample (pixel, s) runs drand48's own
+// generator (x = a x + c mod 2^48, draw = x / 2^48; the reference's drand48,
+// main.cpp:305-306, camera.h:45-53, material.h:44-118) from x0 = key mod 2^48, key =
+// mix64(seed_key ^ (pixel << 32 | s)); constant_medium draws come from a second keyed
+// stream.  Random access for the cooperative samplers: x_{n+j} = A_j x_n + C_j, with
+// (A_j, C_j) from a table (RT_LCG_JUMPS entries, LDS).
 constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
-__device__ __forceinline__ uint64_t mix64_(uint64_t z) {
+constexpr uint64_t kLcgA = 0x5DEECE66Dull, kLcgC = 0xBull, kLcgM = 0xFFFFFFFFFFFFull;
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-#ifdef RT_PROBE_MIX
-}  // namespace
-__device__ uint64_t rt_probe_zero;   // timing probe only: a second mix64 per call, masked by a run-time 0
-namespace {
-__device__ __forceinline__ uint64_t mix64(uint64_t z) { return mix64_(z) ^ (mix64_(z ^ 0x1234567ull) & rt_probe_zero); }
-#else
-__device__ __forceinline__ uint64_t mix64(uint64_t z) { return mix64_(z); }
-#endif
 // (z >> 16) * 2^-48, built as the double 1 + (z >> 16) * 2^-48 (the 48 bits as the
 // top of the 52-bit mantissa) minus 1: both steps exact, so the same value as the
 // integer conversion, for one f64 add instead of two conversions, a scale and an add.
@@ -91,6 +88,47 @@ __device__ __forceinline__ double u48(uint64_t z) {
     const uint64_t bits = 0x3FF0000000000000ull | ((z >> 12) & 0x000FFFFFFFFFFFF0ull);
     return __longlong_as_double((long long)bits) - 1.0;
 }
+// x * 2^-48 for a 48-bit state, the same way
+__device__ __forceinline__ double u48x(uint64_t x) {
+    return __longlong_as_double((long long)(0x3FF0000000000000ull | (x << 4))) - 1.0;
+}
+// One drand48 step, mod 2^48 with 32-bit operations: a = 5 * 2^32 + 0xDEECE66D, x =
+// xh * 2^32 + xl (xh < 2^16), so a x = 0xDEECE66D xl + (5 xl + 0xDEECE66D xh) 2^32
+// (mod 2^48): one v_mad_u64_u32 (+ c), two 32-bit multiply-adds into the high word.
+__device__ __forceinline__ uint64_t lcg_step(uint64_t x) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint64_t p = (uint64_t)xl * 0xDEECE66Du + kLcgC;
+    const uint32_t hi = (uint32_t)(p >> 32) + xl * 5u + xh * 0xDEECE66Du;
+    return ((uint64_t)(hi & 0xFFFFu) << 32) | (uint32_t)p;
+}
+// j steps at once: x_{n+j} = A_j x_n + C_j (mod 2^48); jt = (A_j lo, A_j hi, C_j lo, C_j hi)
+typedef unsigned U4j __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint64_t lcg_jump(uint64_t x, U4j jt) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint64_t p = (uint64_t)xl * jt.x + (((uint64_t)jt.w << 32) | jt.z);   // wraps mod 2^64: only 48 bits kept
+    const uint32_t hi = (uint32_t)(p >> 32) + xl * jt.y + xh * jt.x;
+    return ((uint64_t)(hi & 0xFFFFu) << 32) | (uint32_t)p;
+}
+// Jumps of 0 .. RT_LCG_JUMPS - 1 steps: a cooperative round's candidate t of an owner
+// drawing K per candidate starts K t <= 3 * 63 steps on, and an owner advances by K
+// tried <= 3 * 64 (coop_reject).
+#define RT_LCG_JUMPS 193
+struct LcgJumpTable {
+    U4j e[RT_LCG_JUMPS];
+    constexpr LcgJumpTable() : e() {
+        uint64_t A = 1, C = 0;
+        for (int j = 0; j < RT_LCG_JUMPS; ++j) {
+            e[j] = U4j{(uint32_t)A, (uint32_t)(A >> 32), (uint32_t)C, (uint32_t)(C >> 32)};
+            A = (A * kLcgA) & kLcgM;
+            C = (C * kLcgA + kLcgC) & kLcgM;
+        }
+    }
+};
+__constant__ const LcgJumpTable kLcgJump = LcgJumpTable();
+typedef __attribute__((address_space(3))) const U4j LdsJump;   // the table's LDS copy (ds_read_b128)
+// two steps (a new sample's jitter draws, taken from its pre-made start)
+constexpr uint64_t kLcgA2 = (kLcgA * kLcgA) & kLcgM, kLcgC2 = (kLcgA * kLcgC + kLcgC) & kLcgM;
+
 // key of sample (pixel, sample): mix64(seed_key ^ (pixel << 32 | sample)) with
 // seed_key = mix64(seed ^ 0x5851F42D4C957F2D), computed once per launch
 __device__ __forceinline__ uint64_t seed_key(uint64_t seed) { return mix64(seed ^ 0x5851F42D4C957F2Dull); }
@@ -98,11 +136,14 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t skey, uint32_t pixel, ui
     return mix64(skey ^ (((uint64_t)pixel << 32) | sample));
 }
 struct Rng {
-    uint64_t ctr;    // key + n*GAMMA for the last draw n (n = 0 after start)
+    uint64_t x;      // the sample's drand48 state
     uint64_t mkey;   // medium stream key, derived once per sample
-    __device__ __forceinline__ void start(uint64_t k) { ctr = k; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
-    __device__ __forceinline__ double next() { ctr += kGamma; return u48(mix64(ctr)); }
-    __device__ __forceinline__ void skip() { ctr += kGamma; }   // a draw whose value is not used
+    __device__ __forceinline__ void start(uint64_t k) { x = k & kLcgM; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
+    __device__ __forceinline__ double next() { x = lcg_step(x); return u48x(x); }
+    __device__ __forceinline__ void skip() { x = lcg_step(x); }   // a draw whose value is not used
+    __device__ __forceinline__ void skip2() {                     // two of them
+        x = lcg_jump(x, U4j{(uint32_t)kLcgA2, (uint32_t)(kLcgA2 >> 32), (uint32_t)kLcgC2, (uint32_t)(kLcgC2 >> 32)});
+    }
     __device__ __forceinline__ double medium(int bounce, int k) const {
         uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
         return u48(mix64(mkey + (m + 1) * kGamma));
@@ -797,15 +838,15 @@ __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, 
 // candidate's first draw.
 struct SphereCand {   // material.h:41-47 random_in_unit_sphere
     __device__ __forceinline__ bool operator()(uint64_t base, V3 &p) const {
-        const double x = u48(mix64(base + kGamma)), y = u48(mix64(base + 2 * kGamma)), z = u48(mix64(base + 3 * kGamma));
-        p = sub(scale(2.0f, mk((float)x, (float)y, (float)z)), mk(1, 1, 1));
+        const uint64_t x1 = lcg_step(base), x2 = lcg_step(x1), x3 = lcg_step(x2);
+        p = sub(scale(2.0f, mk((float)u48x(x1), (float)u48x(x2), (float)u48x(x3))), mk(1, 1, 1));
         return (double)dot(p, p) < 1.0;
     }
 };
 struct DiskCand {     // camera.h:6-12 random_in_unit_disk
     __device__ __forceinline__ bool operator()(uint64_t base, V3 &p) const {
-        const double a = u48(mix64(base + kGamma)), b = u48(mix64(base + 2 * kGamma));
-        p = sub(scale(2.0f, mk((float)a, (float)b, 0)), mk(1, 1, 0));
+        const uint64_t x1 = lcg_step(base), x2 = lcg_step(x1);
+        p = sub(scale(2.0f, mk((float)u48x(x1), (float)u48x(x2), 0)), mk(1, 1, 0));
         return (double)dot(p, p) < 1.0;
     }
 };
@@ -859,7 +900,8 @@ __constant__ const CoopTable kCoop = CoopTable();
 // candidate costs every lane more than the saved rounds).  Candidate position
 // c = lane belongs to slot c mod m as that owner's candidate c / m.
 template <int K, bool kCount, class Cand>
-__device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, uint32_t lane, Counters &cnt, Cand cand) {
+__device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, const LdsJump *jt, uint32_t lane,
+                                          Counters &cnt, Cand cand) {
     V3 res = mk(0, 0, 0);
     bool pending = want;
     uint64_t U = wballot(pending);
@@ -868,13 +910,13 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
         const uint32_t inv = kCoop.inv[m];
         const uint64_t P = kCoop.stride_mask[m];               // lanes congruent to 0 mod m
         const uint32_t r = lanes_below(U);
-        if (pending) slots[r].ctr = g.ctr;
+        if (pending) slots[r].ctr = g.x;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t t = (lane * inv) >> 16;                 // lane / m
         const uint32_t slot = lane - t * m;
-        const uint64_t base = slots[slot].ctr + (uint64_t)(K * t) * kGamma;
+        const uint64_t base = lcg_jump(slots[slot].ctr, jt[K * t]);   // the owner's state before candidate t
         V3 p;
         const uint64_t okm = wballot(cand(base, p));
         if (kCount && first_active()) cnt.w_rius++;
@@ -886,7 +928,7 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
             src = won ? (uint32_t)__builtin_ctzll(win) : lane;
             // candidates consumed: up to the winner, or all of the owner's this round
             const uint32_t tried = ((won ? src : 63u - r) * inv >> 16) + 1u;
-            g.ctr += (uint64_t)(K * tried) * kGamma;
+            g.x = lcg_jump(g.x, jt[K * tried]);
             if (kCount) cnt.l_rius += tried;
             pending = !won;
         }
@@ -910,8 +952,8 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, ui
 // exactly those of coop_reject<2> / coop_reject<3>.  Lets the megakernel run the
 // lens-disk candidates of new camera samples in the shading stage's rounds.
 template <bool kCount>
-__device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, CoopSlot *slots, uint32_t lane,
-                                                Counters &cnt) {
+__device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, CoopSlot *slots, const LdsJump *jt,
+                                                uint32_t lane, Counters &cnt) {
     V3 res = mk(0, 0, 0);
     bool pending = want;
     const uint32_t K = disk ? 2u : 3u;
@@ -921,17 +963,16 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
         const uint32_t inv = kCoop.inv[m];
         const uint64_t P = kCoop.stride_mask[m];               // lanes congruent to 0 mod m
         const uint32_t r = lanes_below(U);
-        if (pending) { slots[r].ctr = g.ctr; slots[r].pad = K; }
+        if (pending) { slots[r].ctr = g.x; slots[r].pad = K; }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint32_t t = (lane * inv) >> 16;                 // lane / m
         const uint32_t slot = lane - t * m;
         const uint32_t kk = (uint32_t)slots[slot].pad;
-        const uint64_t base = slots[slot].ctr + (uint64_t)(kk * t) * kGamma;
-        const double x = u48(mix64(base + kGamma)), y = u48(mix64(base + 2 * kGamma)), z = u48(mix64(base + 3 * kGamma));
-        const float pz = kk == 3u ? 2.0f * (float)z - 1.0f : 0.0f;
-        const V3 p = mk(2.0f * (float)x - 1.0f, 2.0f * (float)y - 1.0f, pz);
+        const uint64_t x1 = lcg_step(lcg_jump(slots[slot].ctr, jt[kk * t])), x2 = lcg_step(x1), x3 = lcg_step(x2);
+        const float pz = kk == 3u ? 2.0f * (float)u48x(x3) - 1.0f : 0.0f;
+        const V3 p = mk(2.0f * (float)u48x(x1) - 1.0f, 2.0f * (float)u48x(x2) - 1.0f, pz);
         const uint64_t okm = wballot((double)dot(p, p) < 1.0);
         if (kCount && first_active()) cnt.w_rius++;
         uint32_t src = lane;
@@ -941,7 +982,7 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
             won = win != 0ull;
             src = won ? (uint32_t)__builtin_ctzll(win) : lane;
             const uint32_t tried = ((won ? src : 63u - r) * inv >> 16) + 1u;
-            g.ctr += (uint64_t)(K * tried) * kGamma;
+            g.x = lcg_jump(g.x, jt[K * tried]);
             if (kCount) cnt.l_rius += tried;
             pending = !won;
         }

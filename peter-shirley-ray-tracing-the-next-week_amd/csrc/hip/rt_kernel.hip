@@ -82,6 +82,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ CamV4 lds_cam[6];
+    __shared__ U4j lds_jump[RT_LCG_JUMPS];   // drand48 jump-ahead table (coop_reject)
     // per wave: the next RT_PRE work items' sample starts, made 64 at a time (refill)
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
@@ -98,6 +99,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // the media records are read from LDS (one broadcast read per medium)
     load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) store_camera(A, lds_cam);
+    for (uint32_t i = threadIdx.x; i < RT_LCG_JUMPS; i += kBlock) lds_jump[i] = kLcgJump.e[i];
+    const LdsJump *jt = (const LdsJump *)lds_jump;
     if (kLds) {
         // interior child references become byte offsets into the planes (n * 16): a
         // node step's LDS address is then the reference itself (LdsNodes)
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     r.o = mk(0, 0, 0); r.d = mk(0, 0, 0); r.time = 0;
     V3 beta = mk(1, 1, 1);
     int depth = 0;
-    Rng g; g.ctr = 0; g.mkey = 0;
+    Rng g; g.x = 0; g.mkey = 0;
     // this lane's pre-made sample start, taken by retire_and_claim for camera_begin
     // (read out at once: a refill later in the same claim reuses the slots)
     bool pre_have = false;
@@ -214,8 +217,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const int x = (int)(xy & 0xFFFFu), j = A.ny - 1 - (int)(xy >> 16);
             const uint64_t K = sample_key(skey, (uint32_t)(j * A.nx + x), c * (uint32_t)A.chunk + A.sample_offset);
             // main.cpp:305-306; A.rnx = RN(1/float(nx)) from the host (div_rn)
-            const float cu = div_rn((float)((double)x + u48(mix64(K + kGamma))), (float)A.nx, A.rnx);
-            const float cv = div_rn((float)((double)j + u48(mix64(K + 2 * kGamma))), (float)A.ny, A.rny);
+            const uint64_t x1 = lcg_step(K & kLcgM), x2 = lcg_step(x1);   // the sample's first two draws
+            const float cu = div_rn((float)((double)x + u48x(x1)), (float)A.nx, A.rnx);
+            const float cv = div_rn((float)((double)j + u48x(x2)), (float)A.ny, A.rny);
             pre_key[lane] = K;
             pre_uv[lane] = make_float2(cu, cv);
         }
@@ -270,8 +274,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (starting) {
             if (pre_have) {   // a work item's first sample: made by refill
                 g.start(pre_k);
-                g.skip();
-                g.skip();   // the two jitter draws
+                g.skip2();   // the two jitter draws
                 cu_ = pre_cuv.x;
                 cv_ = pre_cuv.y;
                 pre_have = false;
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const bool starting = phase == PH_IDLE && !finished;
             float cu_ = 0, cv_ = 0;
             camera_begin(starting, cu_, cv_);
-            const V3 disk = coop_reject<2, kCount>(starting, g, slots, lane, cnt, DiskCand());
+            const V3 disk = coop_reject<2, kCount>(starting, g, slots, jt, lane, cnt, DiskCand());
             camera_finish(starting, cu_, cv_, disk);
         }
         mark(0);
@@ -469,7 +472,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         float cu_ = 0, cv_ = 0;
         camera_begin(starting, cu_, cv_);
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
-        const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, lane, cnt);
+        const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, jt, lane, cnt);
         if (ready && !ends) {
             const ShadeOut so = shade_finish(A, ready, have, r, rd, hr, st, pt, g);
             if (so.scattered) {
@@ -656,5 +659,5 @@ extern "C" int rt_megakernel_lds_static_actual(void) {
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 +
-                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8)) + 256;
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8) + RT_LCG_JUMPS * 16) + 256;
 }
