@@ -69,6 +69,7 @@ struct RtKernelArgs {
     float4 *slab;             // [nchunks][npix] partial sums of this launch's sample batch
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)
+    unsigned long long *wave_log;   // profile variant, RTNW_WAVE_LOG: per wave (start, dry, end, hw id, items)
 };
 
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);

@@ -164,6 +164,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // wave timeline (kProf): start, first sight of the empty pool, end (s_memrealtime: one clock for all CUs)
     const uint64_t rt_start = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t rt_exhaust = 0;
+    uint32_t rt_items = 0;   // work items this wave claimed (kProf)
     auto mark = [&](int k) {
         if (kProf) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             pool_end = min(base + size, A.nitems);
         }
         const uint32_t n = min(64u, pool_end - pool_next);
+        if (kProf) rt_items += n;
         if (lane < n) {
             const uint32_t it = pool_next + lane;
             const uint32_t c = it / A.npix;
@@ -519,6 +521,16 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         atomicMax(&T[4], rt_end);
         atomicAdd(&T[5], rt_end - (unsigned long long)rt_start);
         atomicAdd(&T[6], 1ull);
+        if (A.wave_log) {   // HW_ID (cu, simd, wave slot, se) and XCC_ID through s_getreg (reads)
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+            unsigned long long *W = A.wave_log + 5 * ((size_t)blockIdx.x * (kBlock / 64) + wave);
+            W[0] = rt_start;
+            W[1] = rt_exhaust ? rt_exhaust : rt_end;
+            W[2] = rt_end;
+            W[3] = ((unsigned long long)xcc << 32) | hw;
+            W[4] = rt_items;
+        }
     }
     if (kCount) {
         uint64_t w[5] = {cnt.w_iters, cnt.w_nodes, cnt.w_prims, cnt.w_rius, cnt.l_rius};

@@ -731,6 +731,14 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.slab = (float4 *)s->slab;
     a.counter = (uint32_t *)s->counter;
     a.stats = (unsigned long long *)s->stats;
+    // RTNW_WAVE_LOG=<file> with RT_FLAG_PROFILE: every wave's timeline appended to the
+    // file as 5 uint64 (start, pool dry, end in s_memrealtime ticks, xcc << 32 | HW_ID,
+    // items claimed) per wave and batch (tools/tail_probe.py --wave-log; diagnostics)
+    const char *wave_log_path = prof ? std::getenv("RTNW_WAVE_LOG") : nullptr;
+    unsigned long long *wave_log = nullptr;
+    const size_t wave_log_n = (size_t)s->grid[2] * ((s->lds_nodes ? RT_LDS_BLOCK : RT_BLOCK) / 64) * 5;
+    if (wave_log_path) HIP_TRY(hipMalloc(&wave_log, wave_log_n * sizeof(unsigned long long)));
+    a.wave_log = wave_log;
 
     // vec3::operator/= (vec3.h:134-141): col *= float(1.0 / ns)
     const uint32_t ns_total = sum_in ? p->sample_offset + (uint32_t)p->spp : (uint32_t)p->spp;
@@ -771,6 +779,14 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, a.nchunks, k, (float4 *)s->acc, rmode,
                                   (const uint32_t *)s->job_out, out_dev, stream));
         HIP_TRY(hipEventRecord(s->ev[2], stream));
+        if (wave_log) {
+            std::vector<unsigned long long> h(wave_log_n);
+            HIP_TRY(hipMemcpy(h.data(), wave_log, h.size() * sizeof h[0], hipMemcpyDeviceToHost));
+            if (FILE *f = std::fopen(wave_log_path, "ab")) {
+                std::fwrite(h.data(), sizeof h[0], h.size(), f);
+                std::fclose(f);
+            }
+        }
         if (stats) {   // one batch at a time: the events are reused
             HIP_TRY(hipEventSynchronize(s->ev[2]));
             float ms0 = 0, ms1 = 0;
@@ -781,6 +797,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         }
     }
 
+    if (wave_log) (void)hipFree(wave_log);
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         stats->samples = (double)s->npix * (double)p->spp;
