@@ -737,7 +737,10 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     const char *wave_log_path = prof ? std::getenv("RTNW_WAVE_LOG") : nullptr;
     unsigned long long *wave_log = nullptr;
     const size_t wave_log_n = (size_t)s->grid[2] * ((s->lds_nodes ? RT_LDS_BLOCK : RT_BLOCK) / 64) * 5;
-    if (wave_log_path) HIP_TRY(hipMalloc(&wave_log, wave_log_n * sizeof(unsigned long long)));
+    if (wave_log_path) {
+        HIP_TRY(hipMalloc(&wave_log, wave_log_n * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(wave_log, 0, wave_log_n * sizeof(unsigned long long), stream));
+    }
     a.wave_log = wave_log;
 
     // vec3::operator/= (vec3.h:134-141): col *= float(1.0 / ns)
@@ -780,8 +783,9 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
                                   (const uint32_t *)s->job_out, out_dev, stream));
         HIP_TRY(hipEventRecord(s->ev[2], stream));
         if (wave_log) {
-            std::vector<unsigned long long> h(wave_log_n);
-            HIP_TRY(hipMemcpy(h.data(), wave_log, h.size() * sizeof h[0], hipMemcpyDeviceToHost));
+            std::vector<unsigned long long> h(wave_log_n);   // the render stream may be non-blocking
+            HIP_TRY(hipMemcpyAsync(h.data(), wave_log, h.size() * sizeof h[0], hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
             if (FILE *f = std::fopen(wave_log_path, "ab")) {
                 std::fwrite(h.data(), sizeof h[0], h.size(), f);
                 std::fclose(f);

@@ -40,7 +40,11 @@ def main():
     sc.render_tile(cam, p, 0, 0, 8, 8)   # warm (a small job; its log is discarded)
     os.remove(path)
     _, st = sc.render_tile(cam, p, 0, 0, nx, ny, stats=True)
-    w = np.fromfile(path, dtype=np.uint64).reshape(-1, 5)
+    raw = np.fromfile(path, dtype=np.uint64)
+    if args.out:
+        raw.tofile(os.path.splitext(args.out)[0] + ".bin")
+    w = raw.reshape(-1, 5)
+    print("records", len(w), "zero starts", int((w[:, 0] == 0).sum()), "first", w[:3].tolist(), file=sys.stderr)
     t0 = w[:, 0].min()
     start, dry, end = [(w[:, k] - t0).astype(np.float64) * 0.01 for k in range(3)]   # us
     xcc = (w[:, 3] >> np.uint64(32)).astype(np.int64) & 0xF
