@@ -126,8 +126,6 @@ struct LcgJumpTable {
 };
 __constant__ const LcgJumpTable kLcgJump = LcgJumpTable();
 typedef __attribute__((address_space(3))) const U4j LdsJump;   // the table's LDS copy (ds_read_b128)
-// two steps (a new sample's jitter draws, taken from its pre-made start)
-constexpr uint64_t kLcgA2 = (kLcgA * kLcgA) & kLcgM, kLcgC2 = (kLcgA * kLcgC + kLcgC) & kLcgM;
 
 // key of sample (pixel, sample): mix64(seed_key ^ (pixel << 32 | sample)) with
 // seed_key = mix64(seed ^ 0x5851F42D4C957F2D), computed once per launch
@@ -141,9 +139,8 @@ struct Rng {
     __device__ __forceinline__ void start(uint64_t k) { x = k & kLcgM; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
     __device__ __forceinline__ double next() { x = lcg_step(x); return u48x(x); }
     __device__ __forceinline__ void skip() { x = lcg_step(x); }   // a draw whose value is not used
-    __device__ __forceinline__ void skip2() {                     // two of them
-        x = lcg_jump(x, U4j{(uint32_t)kLcgA2, (uint32_t)(kLcgA2 >> 32), (uint32_t)kLcgC2, (uint32_t)(kLcgC2 >> 32)});
-    }
+    __device__ __forceinline__ void skip2() { x = lcg_step(lcg_step(x)); }   // two of them (a constant jump's
+                                                                            // 64-bit addend got hoisted and spilled)
     __device__ __forceinline__ double medium(int bounce, int k) const {
         uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
         return u48(mix64(mkey + (m + 1) * kGamma));
@@ -160,7 +157,10 @@ struct Rng {
 // so next to 1 the result is r + r^2 p(r) with r = x - 1 exact: relatively accurate
 // without glibc's separate near-1 path (a branch nearly every wave took for some lane).
 // About 25 double operations instead of ocml's ~100.
-__host__ __device__ __forceinline__ double log_f64(double x) {
+// c02 = 0.2, the polynomial's one coefficient that is neither an inline constant nor
+// folded: the megakernel passes it from LDS (read at the call), since as an immediate
+// the compiler kept it in two VGPRs across the whole persistent loop and spilled them.
+__host__ __device__ __forceinline__ double log_f64(double x, double c02 = 0.2) {
     if (!(x > 0.0)) return -__builtin_huge_val();
     uint64_t ix;
     __builtin_memcpy(&ix, &x, 8);
@@ -179,7 +179,7 @@ __host__ __device__ __forceinline__ double log_f64(double x) {
     const double lo = (w - hi) + r + __builtin_fma(kd, ln2_lo, T[2]);
     const double r2 = r * r;
     double q = __builtin_fma(r, 1.0 / 7, -1.0 / 6);
-    q = __builtin_fma(q, r, 0.2);
+    q = __builtin_fma(q, r, c02);
     q = __builtin_fma(q, r, -0.25);
     q = __builtin_fma(q, r, 1.0 / 3);
     q = __builtin_fma(q, r, -0.5);
@@ -1110,6 +1110,11 @@ __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const
 }
 
 // ------------------------------------------------------------------ media
+// Constants the media stage reads from LDS (rt_megakernel fills them at launch): a
+// volatile read at each use, so the compiler neither hoists them into registers held
+// across the persistent loop (where they were spilled to scratch) nor folds them back.
+struct MediaConsts { double c02; };   // log_f64's 0.2
+typedef __attribute__((address_space(3))) const volatile MediaConsts LdsMediaConsts;
 // constant_medium::hit for every medium after the surface search
 // (constant_medium.h:26-50): the boundary's entry/exit, clipped to [t_min, best]
 // (best = the surface hit, if any), and the free-flight distance from the
@@ -1141,7 +1146,7 @@ __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds
 template <bool kCount, bool kInst = true>
 __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, const Recip &rd,
                                            const Recip &ra, int depth, const Rng &g, bool &have, float &best_t,
-                                           int &med_mat, Counters &cnt) {
+                                           int &med_mat, LdsMediaConsts *mc, Counters &cnt) {
     const float dlen = rd.a;
     if (kCount) cnt.media++;
     const int4 md = M.md;
@@ -1184,7 +1189,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     r1 = r1 < 0 ? 0.f : r1;
     const float distance_inside_boundary = (r2 - r1) * dlen;
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
-    const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k)));
+    const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k), mc->c02));
     const bool hit = ok && hit_distance < distance_inside_boundary;
     const float tm = r1 + div_by(hit_distance, rd);
     best_t = hit ? tm : best_t;
@@ -1197,8 +1202,8 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
 // choosing per medium between the two made the compiler select the address and
 // issue generic (flat) loads, which wait on both memory counters.
 template <bool kCount, bool kInst = true>
-__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, const Ray &r, const Recip &rd,
-                                         int depth, const Rng &g, bool &have, float &best_t, Counters &cnt) {
+__device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, LdsMediaConsts *mc, const Ray &r,
+                                         const Recip &rd, int depth, const Rng &g, bool &have, float &best_t, Counters &cnt) {
     // a = |d|^2 of the boundary spheres' quadratics (sphere.h:28), its reciprocal once for all media
     const Recip ra = recip_of(dot(r.d, r.d), true);
     typedef unsigned U4v __attribute__((ext_vector_type(4)));
@@ -1212,14 +1217,14 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
         M.md = make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
         M.g0 = make_float4(__uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w));
         M.mm = make_float4(__uint_as_float(z.x), __uint_as_float(z.y), __uint_as_float(z.z), __uint_as_float(z.w));
-        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, mc, cnt);
     }
     for (int k = RT_LDS_MEDIA; k < A.nmedia; ++k) {
         MediumRec M;
         M.md = A.media[k];
         M.g0 = A.bprims[M.md.x * 4 + 0];
         M.mm = A.bprims[M.md.x * 4 + 1];
-        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, cnt);
+        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, mc, cnt);
     }
     return med_mat;
 }

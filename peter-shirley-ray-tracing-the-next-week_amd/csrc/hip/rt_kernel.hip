@@ -82,6 +82,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
     __shared__ MediumRec lds_media[RT_LDS_MEDIA];
     __shared__ CamV4 lds_cam[6];
+    __shared__ MediaConsts lds_mconst;
     __shared__ U4j lds_jump[RT_LCG_JUMPS];   // drand48 jump-ahead table (coop_reject)
     // per wave: the next RT_PRE work items' sample starts, made 64 at a time (refill)
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
@@ -98,7 +99,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     float2 *pre_uv = lds_pre_uv[wave];
     // the media records are read from LDS (one broadcast read per medium)
     load_media<kBlock>(A, lds_media);
-    if (threadIdx.x == 0) store_camera(A, lds_cam);
+    if (threadIdx.x == 0) {
+        store_camera(A, lds_cam);
+        lds_mconst.c02 = 0.2;
+    }
     for (uint32_t i = threadIdx.x; i < RT_LCG_JUMPS; i += kBlock) lds_jump[i] = kLcgJump.e[i];
     const LdsJump *jt = (const LdsJump *)lds_jump;
     if (kLds) {
@@ -450,7 +454,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            const int med_mat = media_hit<kCount, kInst>(A, lds_media, r, rd, depth, g, have, best_t, cnt);
+            const int med_mat = media_hit<kCount, kInst>(A, lds_media, (LdsMediaConsts *)&lds_mconst, r, rd, depth, g, have,
+                                                         best_t, cnt);
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);
@@ -670,6 +675,6 @@ extern "C" int rt_megakernel_lds_static_actual(void) {
 
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
-    return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 +
+    return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 + 16 +
                  (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8) + RT_LCG_JUMPS * 16) + 256;
 }
