@@ -183,12 +183,32 @@ def lib_sha16():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
+def kernel_sha16(path=None):
+    """SHA-256 (16 hex) of the library's device code object (its `.hip_fatbin`
+    section): the PMC counters of a committed profile depend on the kernels only, so a
+    profile stays this build's when only host code changed."""
+    import struct
+    with open(path or rtnw.LIB_PATH, "rb") as f:
+        b = f.read()
+    if b[:4] != b"\x7fELF" or b[4] != 2:
+        return None
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names = secs[shstrndx][4]
+    for sec in secs:
+        name = b[names + sec[0]: b.index(b"\0", names + sec[0])]
+        if name == b".hip_fatbin":
+            return hashlib.sha256(b[sec[4]: sec[4] + sec[5]]).hexdigest()[:16]
+    return None
+
+
 def read_profile(workload_key, sha=None):
     """The committed PMC summary (profiles/r<NN>/traffic.json, tools/pmc_traffic.py
     from separate rocprofv3 passes of this workload): HBM bytes and VALU instructions
-    per sample of the timed megakernel, and the library build they were measured on.
-    The summary of this very build (lib_sha16 == sha) if one is committed, else the
-    latest round's (profile_matches_library then says false)."""
+    per sample of the timed megakernel, and the kernels they were measured on.  The
+    summary of these very kernels (kernel_sha16 == sha, the device code object) if one
+    is committed, else the latest round's (profile_matches_library then says false)."""
     found = []
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "**", "traffic.json"), recursive=True)):
         try:
@@ -201,7 +221,7 @@ def read_profile(workload_key, sha=None):
             found.append(t)
     if not found:
         return None
-    same = [t for t in found if sha and t.get("lib_sha16") == sha]
+    same = [t for t in found if sha and (t.get("kernel_sha16") == sha or t.get("lib_sha16") == sha)]
     return (same or found)[-1]
 
 
@@ -396,7 +416,7 @@ def main():
                             flags=rtnw.RT_FLAG_COUNT)
     cst = scene.render_tiles(cam, cnt, tiles, out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream, stats=True)
     cache_bytes = cst["algorithmic_bytes"]
-    sha = lib_sha16()
+    sha = kernel_sha16() or lib_sha16()
     # the PMC profile of this config (c5 on several GPUs: c4's, whose per-sample wave
     # coherence is the closer one — an interleaved rank's 8x8 work block spans 32x16
     # pixels of the 1000^2 view, against 8x8 of c4's 500^2 and 8x8 of c5's on one GPU)
@@ -435,7 +455,7 @@ def main():
                     "L1/L2 hits)"}
     if prof:
         roof["profile"] = prof["path"]
-        roof["profile_matches_library"] = prof.get("lib_sha16") == sha
+        roof["profile_matches_library"] = sha in (prof.get("kernel_sha16"), prof.get("lib_sha16"))
         if prof.get("valu_insts_per_sample"):
             vi = prof["valu_insts_per_sample"] * rank_samples
             roof["valu_insts_per_sample"] = prof["valu_insts_per_sample"]

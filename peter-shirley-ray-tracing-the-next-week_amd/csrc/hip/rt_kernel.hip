@@ -30,6 +30,7 @@
 // with -ffp-contract=off so no FMA is introduced where the reference has none (the
 // BVH slab test, which decides nothing about the result, uses explicit fmaf).
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "rt_device.h"
@@ -599,11 +600,21 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
     size_t dyn = 0;
     if (kLds == 1) {
         dyn = RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES(a->stack_depth);
-        // dynamic LDS above the default limit: the attribute is set on the current
-        // device's function before every launch (cheap, and right for any device and
-        // any thread, where a once-per-process flag is not)
-        hipError_t e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        // Dynamic LDS above the default limit: the attribute (the most any scene can
+        // ask for) is set once per device and variant, recorded in an atomic bit mask
+        // (thread-safe; calling hipFuncSetAttribute before every launch cost ~0.6 ms
+        // of host time per render step).
+        static std::atomic<uint64_t> done{0};
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
+        const uint64_t bit = 1ull << (dev & 63);
+        if (!(done.load(std::memory_order_acquire) & bit)) {
+            e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    RT_LDS_BUDGET - rt_megakernel_lds_static_bytes());
+            if (e != hipSuccess) return e;
+            done.fetch_or(bit, std::memory_order_release);
+        }
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(kLds == 1 ? RT_LDS_BLOCK : RT_BLOCK), dyn, stream, *a);
     return hipGetLastError();

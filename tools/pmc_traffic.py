@@ -61,8 +61,10 @@ def main():
                        "peter-shirley-ray-tracing-the-next-week_amd", "librt_hip.so")
     with open(lib, "rb") as f:
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
     res = {"config": config, "workload": f"{config} (bench.py --config {config})", "samples_per_launch": samples,
-           "lib_sha16": sha}
+           "lib_sha16": sha, "kernel_sha16": bench.kernel_sha16(lib)}
     if fetch and write:
         fb = fetch["FETCH_SIZE"] * 1024.0
         wb = write["WRITE_SIZE"] * 1024.0
