@@ -370,12 +370,14 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     if (kCount && act) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
                     if (wballot(in) == 0ull) continue;
                     const int first = __builtin_amdgcn_readfirstlane(fbits(gh.x));
-                    const int count = __builtin_amdgcn_readfirstlane(fbits(gh.y));
+                    const int kinds = __builtin_amdgcn_readfirstlane(fbits(gh.w));
+                    const int nyz = __builtin_amdgcn_readfirstlane(fbits(bz.z));
                     const int inst = __builtin_amdgcn_readfirstlane(fbits(gh.z));
                     Ray ro = r;
                     if (kInst && inst >= 0) ro = to_object(A.insts, inst, r);
-                    lockstep_prims<kCount, kInst, false>(P, first, count, A.insts, ro, A.tmin, in, inst, best_t, best_key,
-                                                         best_prim, cnt);
+                    ScanBest b{best_t, best_key, best_prim};
+                    scan_group<kCount, kInst>(P, first, kinds, nyz, inst, ro, A.tmin, in, b, cnt);
+                    best_t = b.t; best_key = b.key; best_prim = b.prim;
                 }
                 if (act) phase = PH_READY;
             }
@@ -416,15 +418,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                                 int key, kind;
                                 float t = prim_t_head<kInst, kK>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
                                 if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                                if (t < best_t || (t == best_t && key < best_key)) {
-                                    best_t = t; best_key = key; best_prim = ia;
-                                }
+                                keep_closest(true, t, key, ia, best_t, best_key, best_prim);
                                 if (two) {
                                     t = prim_t_head<kInst, kK>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
                                     if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                                    if (t < best_t || (t == best_t && key < best_key)) {
-                                        best_t = t; best_key = key; best_prim = ib;
-                                    }
+                                    keep_closest(true, t, key, ib, best_t, best_key, best_prim);
                                 }
                             };
                             // the kinds the wave tests in this pass: a wave of spheres only or of

@@ -391,8 +391,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     if (s->scan) {
         order.resize(d->nprims);
         for (int i = 0; i < d->nprims; i++) order[i] = i;
-        std::stable_sort(order.begin(), order.end(),
-                         [&](int x, int y) { return d->prims[x].instance < d->prims[y].instance; });
+        // by chain, then by kind within a chain (rt_dgroup: one loop per kind)
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+            const rt_prim &px = d->prims[x], &py = d->prims[y];
+            return px.instance != py.instance ? px.instance < py.instance : px.kind < py.kind;
+        });
         for (int i = 0; i < d->nprims; i++) {
             const rt_prim &pr = d->prims[order[i]];
             float lo[3], hi[3];
@@ -407,6 +410,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             }
             rt_dgroup &g = groups.back();
             g.count++;
+            if (pr.kind == RT_PRIM_YZ_RECT) g.nyz++;
+            else g.kinds += 1 << (8 * pr.kind);     // count <= RT_SCAN_MAX < 256 per kind
             g.bx[0] = std::min(g.bx[0], lo[0]); g.bx[1] = std::max(g.bx[1], hi[0]);
             g.bx[2] = std::min(g.bx[2], lo[1]); g.bx[3] = std::max(g.bx[3], hi[1]);
             g.bz[0] = std::min(g.bz[0], lo[2]); g.bz[1] = std::max(g.bz[1], hi[2]);

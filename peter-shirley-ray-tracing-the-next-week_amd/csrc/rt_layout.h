@@ -96,17 +96,21 @@ struct rt_dprim {
 
 // Flat scan (scenes of at most RT_SCAN_MAX surface primitives, capi.cpp): the
 // primitives are ordered by instance chain, and each run of one chain is a group,
-// 48 B: (first, count, instance (-1 none), -) + its world box as in a BVH node,
-// (lo.x, hi.x, lo.y, hi.y), (lo.z, hi.z, -, -).  A wave tests every group's box
+// 48 B: (first, count, instance (-1 none), kinds) + its world box as in a BVH node,
+// (lo.x, hi.x, lo.y, hi.y), (lo.z, hi.z, n_yz, -).  Within a group the primitives
+// are ordered by kind (list order within a kind): kinds = n_sphere | n_moving << 8 |
+// n_xy << 16 | n_xz << 24, then n_yz yz rects.  A wave tests every group's box
 // against all its rays at once, transforms its rays into the group's object space
-// ONCE, and tests the group's primitives in lockstep (every lane the same one):
-// the instance level of a two-level structure, without per-leaf transforms.
+// ONCE, and tests the group's primitives in lockstep (every lane the same one), one
+// loop per kind: the instance level of a two-level structure, without per-leaf
+// transforms or per-primitive kind branches.
 #define RT_SCAN_MAX 64
 // BVH scenes: at most this many of the largest primitives are pre-scanned (capi.cpp).
 #define RT_PRESCAN_MAX 8
 struct rt_dgroup {
-    int32_t first, count, instance, pad;
-    float bx[4], bz[4];
+    int32_t first, count, instance, kinds;
+    float bx[4], bz[2];
+    int32_t nyz, pad;
 };
 
 // Material, 32 B: (kind, texture, fuzz, ref_idx) + (albedo.xyz, flags).  A dielectric
