@@ -238,6 +238,31 @@ __device__ __forceinline__ Ray to_object(const float4 *insts, int inst, Ray r) {
     }
     return r;
 }
+// The same for a wave-uniform chain (flat-scan groups, pre-scanned primitives): the
+// records through the scalar cache (constant address space, uniform index), the op
+// codes in SGPRs and scalar branches, instead of a chain of dependent vector loads.
+typedef float F4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const F4v ConstInst;
+__device__ __forceinline__ Ray to_object_uniform(const float4 *insts, int inst, Ray r) {
+    const ConstInst *I = (const ConstInst *)insts + inst * 7;
+    const int nops = fbits(I[0].x);
+    for (int k = 0; k < nops; ++k) {
+        const F4v op = I[1 + k];
+        const int code = fbits(op.x);
+        if (code == RT_OP_TRANSLATE) {
+            r.o = sub(r.o, mk(op.y, op.z, op.w));
+        } else if (code == RT_OP_ROTATE_Y) {
+            const float s = op.y, c = op.z;
+            V3 o = r.o, d = r.d;
+            o.x = c * r.o.x - s * r.o.z;
+            o.z = s * r.o.x + c * r.o.z;
+            d.x = c * r.d.x - s * r.d.z;
+            d.z = s * r.d.x + c * r.d.z;
+            r.o = o; r.d = d;
+        }
+    }
+    return r;
+}
 
 // Hit point / normal back to world space, innermost wrapper first (hitable.h:43-45, 69, 137-145).
 __device__ __forceinline__ void to_world(const float4 *insts, int inst, V3 &p, V3 &n) {
@@ -594,7 +619,6 @@ __device__ __forceinline__ void cas(float &ka, uint32_t &ca, float &kb, uint32_t
 // global reader fetches them from HBM (L1/L2), the LDS reader from the workgroup's
 // copy, stored as 4 planes of RT_LDS_NODE_CAP float4 so that lanes reading different
 // nodes spread over 16 bank windows instead of 4 (the plane contents: load_signed).
-typedef float F4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const F4v LdsF4;
 __device__ __forceinline__ float4 f4(F4v v) { return make_float4(v.x, v.y, v.z, v.w); }
 struct GlobalNodes {
@@ -1100,7 +1124,7 @@ __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const
         const int kind = __builtin_amdgcn_readfirstlane(fbits(mmv.x)) & 0xff;
         const int inst = kPerPrimInst ? __builtin_amdgcn_readfirstlane(fbits(mmv.z)) : group_inst;
         Ray ro = r;
-        if (kInst && kPerPrimInst && inst >= 0) ro = to_object(insts, inst, r);
+        if (kInst && kPerPrimInst && inst >= 0) ro = to_object_uniform(insts, inst, r);
         float t;
         if (kind == RT_PRIM_SPHERE) {
             t = sphere_t(mk(g0.x, g0.y, g0.z), g0.w, ro, tmin);
@@ -1131,17 +1155,29 @@ __device__ __forceinline__ void scan_keep(float t, int key, int q, bool in, int 
 }
 // plane_t without branches: the in-plane coordinates are computed for every t (an
 // out-of-range t is replaced by RT_INF either way), so one select decides the hit
+#ifndef RT_SCAN_PAIRS
+#define RT_SCAN_PAIRS 1
+#endif
 template <bool kCount>
 __device__ __forceinline__ int scan_rects(const ConstF4 *P, int q, int n, float oa, float da, float oi, float di,
                                           float oj, float dj, float tmin, bool in, int ck, ScanBest &b, Counters &cnt) {
     const int e = q + n;
-    for (; q < e; ++q) {
-        const F4v g0 = P[4 * q], mm = P[4 * q + 1];
+    auto test = [&](F4v g0, F4v mm, int i) {
         const float t = (mm.y - oa) / da;
         const float a = oi + t * di, c = oj + t * dj;
         const bool miss = (t < tmin) | (t > RT_FLT_MAX) | (a < g0.x) | (a > g0.y) | (c < g0.z) | (c > g0.w);
-        scan_keep<kCount>(miss ? RT_INF : t, -1 - fbits(mm.w), q, in, ck, b, cnt);
+        scan_keep<kCount>(miss ? RT_INF : t, -1 - fbits(mm.w), i, in, ck, b, cnt);
+    };
+    if (RT_SCAN_PAIRS) {
+        // two records per scalar-load wait (scalar loads return out of order, so
+        // every use waits for all of them: a pair halves the waits)
+        for (; q + 1 < e; q += 2) {
+            const F4v g0a = P[4 * q], mma = P[4 * q + 1], g0b = P[4 * q + 4], mmb = P[4 * q + 5];
+            test(g0a, mma, q);
+            test(g0b, mmb, q + 1);
+        }
     }
+    for (; q < e; ++q) test(P[4 * q], P[4 * q + 1], q);
     return e;
 }
 // ro: the lanes' rays in the group's object space; kinds / nyz: rt_dgroup's counts

@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     const int nyz = __builtin_amdgcn_readfirstlane(fbits(bz.z));
                     const int inst = __builtin_amdgcn_readfirstlane(fbits(gh.z));
                     Ray ro = r;
-                    if (kInst && inst >= 0) ro = to_object(A.insts, inst, r);
+                    if (kInst && inst >= 0) ro = to_object_uniform(A.insts, inst, r);
                     ScanBest b{best_t, best_key, best_prim};
                     scan_group<kCount, kInst>(P, first, kinds, nyz, inst, ro, A.tmin, in, b, cnt);
                     best_t = b.t; best_key = b.key; best_prim = b.prim;
