@@ -1146,12 +1146,18 @@ __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const
 // quotients (k - o_a) / d_a (aarect.h:51) share the lane's divisor, but a div_rn by
 // a per-run reciprocal (one IEEE division + the wave's range check per run) measured
 // slower than the IEEE division per rect (45.2 vs 45.8 ms): runs hold 1-3 rects.
-struct ScanBest { float t; int key; uint32_t prim; };
+// The scan's closest hit: t and key << 8 | primitive (keys are unique and |key| <=
+// RT_SCAN_MAX, primitives < 256), so one compare and one select carry both.
+struct ScanBest { float t; int kp; };
+static_assert(RT_SCAN_MAX < 256, "ScanBest packs the primitive index in 8 bits");
 template <bool kCount>
 __device__ __forceinline__ void scan_keep(float t, int key, int q, bool in, int ck, ScanBest &b, Counters &cnt) {
     if (kCount && in) cnt.prim(ck);
     if (kCount && first_active()) cnt.w_prims++;
-    keep_closest(in, t, key, (uint32_t)q, b.t, b.key, b.prim);
+    const int kp = key * 256 + q;   // wave-uniform
+    const bool take = in & ((t < b.t) | ((t == b.t) & (kp < b.kp)));
+    b.t = take ? t : b.t;
+    b.kp = take ? kp : b.kp;
 }
 // plane_t without branches: the in-plane coordinates are computed for every t (an
 // out-of-range t is replaced by RT_INF either way), so one select decides the hit
@@ -1168,16 +1174,17 @@ __device__ __forceinline__ int scan_rects(const ConstF4 *P, int q, int n, float 
         const bool miss = (t < tmin) | (t > RT_FLT_MAX) | (a < g0.x) | (a > g0.y) | (c < g0.z) | (c > g0.w);
         scan_keep<kCount>(miss ? RT_INF : t, -1 - fbits(mm.w), i, in, ck, b, cnt);
     };
+    const ConstF4 *p = P + 4 * q;   // a running record pointer: no per-primitive address arithmetic
     if (RT_SCAN_PAIRS) {
         // two records per scalar-load wait (scalar loads return out of order, so
         // every use waits for all of them: a pair halves the waits)
-        for (; q + 1 < e; q += 2) {
-            const F4v g0a = P[4 * q], mma = P[4 * q + 1], g0b = P[4 * q + 4], mmb = P[4 * q + 5];
+        for (; q + 1 < e; q += 2, p += 8) {
+            const F4v g0a = p[0], mma = p[1], g0b = p[4], mmb = p[5];
             test(g0a, mma, q);
             test(g0b, mmb, q + 1);
         }
     }
-    for (; q < e; ++q) test(P[4 * q], P[4 * q + 1], q);
+    if (q < e) test(p[0], p[1], q);
     return e;
 }
 // ro: the lanes' rays in the group's object space; kinds / nyz: rt_dgroup's counts

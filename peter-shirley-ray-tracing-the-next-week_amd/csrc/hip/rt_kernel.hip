@@ -362,10 +362,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 const ConstF4 *P = (const ConstF4 *)A.prims;
                 const ConstF4 *G = (const ConstF4 *)A.groups;
                 const Slab sl = make_slab(r, A.tmin);
+                ScanBest b{best_t, 0x7FFFFFFF};   // a new segment: nothing found yet
                 for (int gi = 0; gi < A.ngroups; ++gi) {
                     const F4v gh = G[3 * gi], bx = G[3 * gi + 1], bz = G[3 * gi + 2];
                     float tn, tf;
-                    box_span(sl, F2{bx.x, bx.y}, F2{bx.z, bx.w}, F2{bz.x, bz.y}, best_t, tn, tf);
+                    box_span(sl, F2{bx.x, bx.y}, F2{bx.z, bx.w}, F2{bz.x, bz.y}, b.t, tn, tf);
                     const bool in = act && tn <= tf;
                     if (kCount && act) { cnt.nodes++; if (first_active()) cnt.w_nodes++; }
                     if (wballot(in) == 0ull) continue;
@@ -375,10 +376,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     const int inst = __builtin_amdgcn_readfirstlane(fbits(gh.z));
                     Ray ro = r;
                     if (kInst && inst >= 0) ro = to_object_uniform(A.insts, inst, r);
-                    ScanBest b{best_t, best_key, best_prim};
                     scan_group<kCount, kInst>(P, first, kinds, nyz, inst, ro, A.tmin, in, b, cnt);
-                    best_t = b.t; best_key = b.key; best_prim = b.prim;
                 }
+                best_t = b.t;
+                if (b.kp != 0x7FFFFFFF) { best_key = b.kp >> 8; best_prim = (uint32_t)(b.kp & 0xff); }
                 if (act) phase = PH_READY;
             }
         } else {
