@@ -66,7 +66,7 @@ struct RtKernelArgs {
     uint32_t claim;           // work items per wave-level claim (a multiple of 64) ...
     uint32_t nbig;            // ... for the first nbig claims; the rest (the launch's tail) claim
     uint32_t claim_tail;      //     claim_tail items each, so that waves run dry together
-    float4 *slab;             // [nchunks][npix] partial sums of this launch's sample batch
+    float *slab;              // [nchunks][npix] partial sums (rgb, rt_slab_floats() floats each) of this batch
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)
     unsigned long long *wave_log;   // profile variant, RTNW_WAVE_LOG: per wave (start, dry, end, hw id, items)
@@ -79,7 +79,9 @@ extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int 
 #define RT_RESOLVE_LAST 2     // the last batch: write out (times k unless RAW), else keep acc
 #define RT_RESOLVE_SUM_IN 4   // out holds the running sums of earlier samples on entry
 #define RT_RESOLVE_RAW 8      // write the sums themselves (checkpoints), not sum * k
-extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
+// floats per partial sum in the slab (3: rgb; RT_SLAB_F4=1 builds the 16-B layout, A/B only)
+extern "C" int rt_slab_floats(void);
+extern "C" hipError_t rt_launch_resolve(const float *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
 // mode: 0 plain, 1 count, 2 profile; width: the scene's RtKernelArgs.bvh_width, 0: the flat-scan kernel
 extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int width);

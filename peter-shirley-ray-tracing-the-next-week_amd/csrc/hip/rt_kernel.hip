@@ -42,6 +42,12 @@ namespace {
 // VGPRs and run 24% slower.
 
 // Shade once this many lanes of a wave have their closest hit (see stage 3).
+// partial sums in the slab: rgb, 12 B per work item (RT_SLAB_F4=1: 16-B records, A/B only)
+#if defined(RT_SLAB_F4) && RT_SLAB_F4
+#define RT_SLAB_FLOATS 4
+#else
+#define RT_SLAB_FLOATS 3
+#endif
 #ifndef RT_READY_BATCH
 #define RT_READY_BATCH 48
 #endif
@@ -244,7 +250,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // the next pre-made sample starts (one global atomic per A.claim items)
     auto retire_and_claim = [&]() {
         if (phase == PH_IDLE && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
-            A.slab[item] = make_float4(part.x, part.y, part.z, 0.f);
+            float *sl = A.slab + (size_t)item * RT_SLAB_FLOATS;   // 12 B per item (16 with RT_SLAB_F4)
+            sl[0] = part.x;
+            sl[1] = part.y;
+            sl[2] = part.z;
             item = 0xFFFFFFFFu;
         }
         bool need = phase == PH_IDLE && !finished && item == 0xFFFFFFFFu;
@@ -562,7 +571,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
 // item), so the image does not depend on how the samples were split into batches
 // (capi.cpp bounds the slab per launch).  The last batch applies `col /= float(ns)`
 // as the reciprocal multiply of vec3.h:134-141.
-__global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ slab, uint32_t npix, int nchunks, float k,
+__global__ __launch_bounds__(256) void rt_resolve(const float *__restrict__ slab, uint32_t npix, int nchunks, float k,
                                                   float4 *__restrict__ acc, int mode,
                                                   const uint32_t *__restrict__ out_index, float *__restrict__ out) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -577,8 +586,8 @@ __global__ __launch_bounds__(256) void rt_resolve(const float4 *__restrict__ sla
     }
 #pragma unroll 8
     for (int c = 0; c < nchunks; ++c) {   // the loads run ahead; the adds stay in sample order
-        float4 v = slab[(size_t)c * npix + p];
-        col = add(col, mk(v.x, v.y, v.z));
+        const float *v = slab + ((size_t)c * npix + p) * RT_SLAB_FLOATS;
+        col = add(col, mk(v[0], v[1], v[2]));
     }
     if (!(mode & RT_RESOLVE_LAST)) {
         acc[p] = make_float4(col.x, col.y, col.z, 0.f);
@@ -649,7 +658,9 @@ extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int 
     return a->lds_nodes ? launch_features<1>(a, grid, mode, stream) : launch_features<0>(a, grid, mode, stream);
 }
 
-extern "C" hipError_t rt_launch_resolve(const float4 *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
+extern "C" int rt_slab_floats(void) { return RT_SLAB_FLOATS; }
+
+extern "C" hipError_t rt_launch_resolve(const float *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
                                         const uint32_t *out_index, float *out, hipStream_t stream) {
     int blocks = (int)((npix + 255) / 256);
     hipLaunchKernelGGL(rt_resolve, dim3(blocks), dim3(256), 0, stream, slab, npix, nchunks, k, acc, mode, out_index, out);

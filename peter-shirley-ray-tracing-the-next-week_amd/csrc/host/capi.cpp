@@ -646,7 +646,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     // Work item = `chunk` samples of one pixel, one by default: short items keep each
     // wave's lanes on neighbouring pixels (a wave deals its claims to lanes as they free
     // up; long items let its pixels drift apart): 16 -> 1 sample per item is 92.2 ->
-    // 81.8 ms on c4.  The partial-sum slab holds one float4 per item
+    // 81.8 ms on c4.  The partial-sum slab holds one rgb (12 B) per item
     // of a launch; a job whose slab would pass the budget runs as several launches
     // over sample batches (whole chunks), and the resolve adds every batch to a
     // per-pixel running sum in sample order — so the sum is the same sequence of
@@ -656,11 +656,12 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     const uint64_t nchunks_total = ((uint64_t)p->spp + chunk - 1) / chunk;
     const uint64_t max_items = 0xFFFFFFFFull - 64;
     if ((uint64_t)s->npix > max_items) return fail(RT_ERR_INVALID, "job too large (pixels >= 2^32)");
-    uint64_t per = std::max<uint64_t>(1, slab_budget() / ((uint64_t)s->npix * 16));
+    const uint64_t item_bytes = 4 * (uint64_t)rt_slab_floats();   // one partial sum (rgb)
+    uint64_t per = std::max<uint64_t>(1, slab_budget() / ((uint64_t)s->npix * item_bytes));
     per = std::min<uint64_t>(per, max_items / s->npix);
     per = std::min<uint64_t>(per, nchunks_total);
     const uint64_t nbatches = (nchunks_total + per - 1) / per;
-    const size_t slab_bytes = (size_t)s->npix * per * 16;
+    const size_t slab_bytes = (size_t)s->npix * per * item_bytes;
     if (slab_bytes > s->slab_bytes) {
         if (s->slab) (void)hipFree(s->slab);
         s->slab = nullptr;
@@ -733,7 +734,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.seed = p->seed;
     a.job_xy = (const uint32_t *)s->job_xy;
     a.npix = s->npix;
-    a.slab = (float4 *)s->slab;
+    a.slab = (float *)s->slab;
     a.counter = (uint32_t *)s->counter;
     a.stats = (unsigned long long *)s->stats;
     // RTNW_WAVE_LOG=<file> with RT_FLAG_PROFILE: every wave's timeline appended to the
@@ -784,7 +785,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         HIP_TRY(hipEventRecord(s->ev[0], stream));
         HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
         HIP_TRY(hipEventRecord(s->ev[1], stream));
-        HIP_TRY(rt_launch_resolve((const float4 *)s->slab, s->npix, a.nchunks, k, (float4 *)s->acc, rmode,
+        HIP_TRY(rt_launch_resolve((const float *)s->slab, s->npix, a.nchunks, k, (float4 *)s->acc, rmode,
                                   (const uint32_t *)s->job_out, out_dev, stream));
         HIP_TRY(hipEventRecord(s->ev[2], stream));
         if (wave_log) {

@@ -280,7 +280,7 @@ def test_config5_image_is_independent_of_rank_count_and_batching(monkeypatch):
     one: each batch is added to the per-pixel running sum in sample order
     (main.cpp:311), so the sums are the same float adds.  Oracle crops pin it."""
     nx, ny, ns, seed = 1000, 1000, 8, 55
-    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(1000 * 1000 * 16 * 2))   # 2 samples per launch for 1e6 pixels
+    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(1000 * 1000 * 12 * 2))   # 2 samples (12-B sums) per launch for 1e6 pixels
     one, b1 = _render_shares("final", nx, ny, ns, 1, seed)
     eight, b8 = _render_shares("final", nx, ny, ns, 8, seed)
     assert b1 == [4.0] and set(b8) == {1.0}, (b1, b8)
@@ -301,7 +301,7 @@ def test_batches_keep_explicit_chunks_whole(monkeypatch):
     same as in one launch."""
     nx, ny, ns = 96, 64, 21
     ref = gpu_render("cornell_box", nx, ny, ns, seed=12, chunk=4)
-    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(nx * ny * 16 * 2))   # 2 chunks (8 samples) per launch
+    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(nx * ny * 12 * 2))   # 2 chunks (8 samples) of 12-B sums per launch
     img, st = gpu_render("cornell_box", nx, ny, ns, seed=12, chunk=4, stats=True)
     assert st["batches"] == 3
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
