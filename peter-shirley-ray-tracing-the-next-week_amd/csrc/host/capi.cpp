@@ -661,6 +661,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     per = std::min<uint64_t>(per, max_items / s->npix);
     per = std::min<uint64_t>(per, nchunks_total);
     const uint64_t nbatches = (nchunks_total + per - 1) / per;
+    per = (nchunks_total + nbatches - 1) / nbatches;   // batches of (nearly) equal size, as many
     const size_t slab_bytes = (size_t)s->npix * per * item_bytes;
     if (slab_bytes > s->slab_bytes) {
         if (s->slab) (void)hipFree(s->slab);
