@@ -1111,8 +1111,8 @@ __device__ __forceinline__ void keep_closest(bool in, float t, int key, uint32_t
 // instance are the same in all lanes (scalar loads and branches), so only
 // the kind's own test runs and no lane idles behind another's traversal.  Lanes
 // with `in` false compute but keep nothing.  kPerPrimInst: each primitive's own
-// instance chain (pre-scan); otherwise the caller transformed `r` for the group.
-typedef __attribute__((address_space(3))) const F4v LdsScan;
+// instance chain; otherwise the caller transformed `r`.  Used by the BVH modes'
+// pre-scan; the flat scan, whose groups are ordered by kind, runs scan_group below.
 typedef __attribute__((address_space(4))) const F4v ConstF4;   // uniform index: scalar (SMEM) loads
 template <bool kCount, bool kInst, bool kPerPrimInst, class PT>
 __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const float4 *insts,
