@@ -444,6 +444,10 @@ def main():
                 "prim_tests": (cst["sphere_tests"] + cst["moving_sphere_tests"] + cst["rect_tests"]
                                - cst["medium_tests"]) / max(1.0, 64 * cst["wave_prim_trips"]),
                 "coop_candidates": cst["lane_sphere_draw_trips"] / max(1.0, 64 * cst["wave_sphere_draw_trips"]),
+                # material scatter branches (shade_finish): lanes that scattered per wave pass,
+                # and the distinct materials a pass ran (branches executed one after another)
+                "scatter": cst["lane_scatters"] / max(1.0, 64 * cst["wave_shade_passes"]),
+                "scatter_materials_per_pass": cst["wave_shade_kinds"] / max(1.0, cst["wave_shade_passes"]),
                 "segments_per_wave_iteration": cst["segments"] / max(1.0, cst["wave_iterations"])},
             "note": "the scene is L2/L1-resident: HBM carries ~1% of peak, the kernel is VALU-issue bound "
                     "(DESIGN.md §5c).  achieved = SQ_INSTS_VALU per sample (committed rocprofv3 pass of this "

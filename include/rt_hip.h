@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+/* 2: rt_stats gained the shading-stage divergence fields (wave_shade_passes ...) */
+#define RT_ABI_VERSION 2
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -212,6 +213,12 @@ typedef struct rt_stats {
     double wave_end_first_us;     /*   the first wave to finish */
     double wave_end_mean_us;      /*   mean wave finish */
     double wave_end_last_us;      /*   the last wave to finish (the launch's end) */
+    double wave_shade_passes;     /* RT_FLAG_COUNT: wave-level passes through the material scatter branches */
+    double wave_shade_kinds;      /*   distinct scatter materials (lambertian/metal/dielectric/isotropic) summed
+                                         over those passes: the branches each pass ran */
+    double lane_scatters;         /*   lanes that scattered (SIMD efficiency = this / 64x wave_shade_passes) */
+    double cycles_scatter;        /* RT_FLAG_PROFILE: wave cycles in the material scatter branches (part of
+                                         cycles_shade) */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */

@@ -457,6 +457,9 @@ struct Counters {
              shades = 0, noise = 0;
     // wave-level trip counts (SIMD efficiency = lane-level count / (64 x wave-level count))
     uint64_t w_iters = 0, w_nodes = 0, w_prims = 0, w_rius = 0, l_rius = 0;
+    // material divergence of the shading stage: wave passes through the scatter
+    // branches, the distinct materials each pass ran, and the lanes that scattered
+    uint64_t w_shade = 0, w_kinds = 0, l_scatter = 0;
     __device__ __forceinline__ void prim(int kind) {
         const int k = kind & 0xff;
         if (k == RT_PRIM_SPHERE) spheres++;

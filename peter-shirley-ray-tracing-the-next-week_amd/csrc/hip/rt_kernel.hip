@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     uint32_t best_prim = 0xFFFFFFFFu;
 
     Counters cnt;
-    uint64_t prof[4] = {0, 0, 0, 0};
+    uint64_t prof[5] = {0, 0, 0, 0, 0};   // claim, traverse, media, shade, of which scatter branches
     uint64_t stamp = kProf ? __builtin_amdgcn_s_memtime() : 0;
     // wave timeline (kProf): start, first sight of the empty pool, end (s_memrealtime: one clock for all CUs)
     const uint64_t rt_start = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -482,6 +482,17 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // in the same cooperative rounds as the scattering lanes' sphere candidates.
         const ShadeState st = shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt);
         const bool ends = shade_ends(ready, have, st);
+        if (kCount) {   // material divergence: the scatter branches this wave pass runs (shade_finish)
+            const bool sc = ready && !ends;
+            if (wballot(sc) != 0ull) {
+                const int kinds = (wballot(sc && st.kind == RT_MAT_LAMBERTIAN) != 0ull) +
+                                  (wballot(sc && st.kind == RT_MAT_METAL) != 0ull) +
+                                  (wballot(sc && st.kind == RT_MAT_DIELECTRIC) != 0ull) +
+                                  (wballot(sc && st.kind == RT_MAT_ISOTROPIC) != 0ull);
+                if (first_active()) { cnt.w_shade++; cnt.w_kinds += (uint64_t)kinds; }
+                if (sc) cnt.l_scatter++;
+            }
+        }
         if (ends) end_path(mul(beta, shade_emitted(A, have, r, rd, st)));
         retire_and_claim();
         const bool starting = phase == PH_IDLE && !finished;
@@ -489,6 +500,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         camera_begin(starting, cu_, cv_);
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
         const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, jt, lane, cnt);
+        mark(3);
         if (ready && !ends) {
             const ShadeOut so = shade_finish(A, ready, have, r, rd, hr, st, pt, g);
             if (so.scattered) {
@@ -500,6 +512,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 end_path(mul(beta, so.emitted));
             }
         }
+        mark(4);
         camera_finish(starting, cu_, cv_, pt);
         mark(3);
 #ifdef RT_PROBE_VALU
@@ -524,10 +537,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
 #endif
     }
     if (kProf && lane == 0) {
-        for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_CNT_N + k], (unsigned long long)prof[k]);
+        // the scatter branches' cycles count in the shade stage too
+        for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_STAT_PROF + k], (unsigned long long)(prof[k] + (k == 3 ? prof[4] : 0)));
+        atomicAdd(&A.stats[RT_STAT_SHADE + 3], (unsigned long long)prof[4]);
         // minima as maxima of the complement (the slots start at 0)
         const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
-        unsigned long long *T = A.stats + RT_CNT_N + 9;
+        unsigned long long *T = A.stats + RT_STAT_TIME;
         atomicMax(&T[0], ~(unsigned long long)rt_start);
         atomicMax(&T[1], ~(unsigned long long)(rt_exhaust ? rt_exhaust : rt_end));
         atomicMax(&T[2], (unsigned long long)(rt_exhaust ? rt_exhaust : rt_end));
@@ -547,11 +562,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
     }
     if (kCount) {
-        uint64_t w[5] = {cnt.w_iters, cnt.w_nodes, cnt.w_prims, cnt.w_rius, cnt.l_rius};
-        for (int k = 0; k < 5; ++k) {
+        uint64_t w[8] = {cnt.w_iters, cnt.w_nodes, cnt.w_prims, cnt.w_rius, cnt.l_rius, cnt.w_shade, cnt.w_kinds, cnt.l_scatter};
+        for (int k = 0; k < 8; ++k) {
             uint64_t x = w[k];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);
-            if (lane == 0 && x) atomicAdd(&A.stats[RT_CNT_N + 4 + k], (unsigned long long)x);
+            if (lane == 0 && x) atomicAdd(&A.stats[k < 5 ? RT_STAT_WAVE + k : RT_STAT_SHADE + (k - 5)], (unsigned long long)x);
         }
     }
 

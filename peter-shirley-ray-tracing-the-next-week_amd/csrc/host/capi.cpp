@@ -566,7 +566,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     }
     trace("device attributes");
     // the work counter (64 B) and the statistics counters in one allocation
-    if ((e = hipMalloc(&s->counter, 64 + (RT_CNT_N + 16) * sizeof(unsigned long long))) != hipSuccess)
+    if ((e = hipMalloc(&s->counter, 64 + RT_STATS_LEN * sizeof(unsigned long long))) != hipSuccess)
         return cleanup(hip_fail(e, "hipMalloc counters"));
     s->stats = (uint8_t *)s->counter + 64;
     trace("counters");
@@ -682,7 +682,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     const bool prof = !count && (p->flags & RT_FLAG_PROFILE) != 0;
     const bool sum_in = (p->flags & RT_FLAG_SUM_IN) != 0, sum_out = (p->flags & RT_FLAG_SUM_OUT) != 0;
     const int mode = count ? 1 : (prof ? 2 : 0);
-    if (count || prof) HIP_TRY(hipMemsetAsync(s->stats, 0, (RT_CNT_N + 16) * sizeof(unsigned long long), stream));
+    if (count || prof) HIP_TRY(hipMemsetAsync(s->stats, 0, RT_STATS_LEN * sizeof(unsigned long long), stream));
 
     RtKernelArgs a{};
     a.nodes = (const float4 *)s->nodes;
@@ -831,22 +831,28 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->noise_evals = (double)c[RT_CNT_NOISE];
             stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)s->npix * (double)nchunks_total, s->bvh_width);
             unsigned long long w[5];
-            HIP_TRY(hipMemcpy(w, (unsigned long long *)s->stats + RT_CNT_N + 4, sizeof w, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(w, (unsigned long long *)s->stats + RT_STAT_WAVE, sizeof w, hipMemcpyDeviceToHost));
             stats->wave_iterations = (double)w[0];
             stats->wave_node_trips = (double)w[1];
             stats->wave_prim_trips = (double)w[2];
             stats->wave_sphere_draw_trips = (double)w[3];
             stats->lane_sphere_draw_trips = (double)w[4];
+            unsigned long long sh[3];
+            HIP_TRY(hipMemcpy(sh, (unsigned long long *)s->stats + RT_STAT_SHADE, sizeof sh, hipMemcpyDeviceToHost));
+            stats->wave_shade_passes = (double)sh[0];
+            stats->wave_shade_kinds = (double)sh[1];
+            stats->lane_scatters = (double)sh[2];
         }
         if (prof) {
-            unsigned long long c[RT_CNT_N + 16];
+            unsigned long long c[RT_STATS_LEN];
             HIP_TRY(hipMemcpy(c, s->stats, sizeof c, hipMemcpyDeviceToHost));
-            stats->cycles_claim = (double)c[RT_CNT_N + 0];
-            stats->cycles_traverse = (double)c[RT_CNT_N + 1];
-            stats->cycles_media = (double)c[RT_CNT_N + 2];
-            stats->cycles_shade = (double)c[RT_CNT_N + 3];
+            stats->cycles_claim = (double)c[RT_STAT_PROF + 0];
+            stats->cycles_traverse = (double)c[RT_STAT_PROF + 1];
+            stats->cycles_media = (double)c[RT_STAT_PROF + 2];
+            stats->cycles_shade = (double)c[RT_STAT_PROF + 3];
+            stats->cycles_scatter = (double)c[RT_STAT_SHADE + 3];
             // wave timeline of the last batch, s_memrealtime at 100 MHz (kernel: kProf)
-            const unsigned long long *T = c + RT_CNT_N + 9;
+            const unsigned long long *T = c + RT_STAT_TIME;
             const double t0 = (double)~T[0], us = 0.01;
             stats->wave_exhaust_first_us = ((double)~T[1] - t0) * us;
             stats->wave_exhaust_last_us = ((double)T[2] - t0) * us;

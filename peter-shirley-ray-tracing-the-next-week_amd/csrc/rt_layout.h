@@ -150,3 +150,12 @@ enum {
     RT_CNT_SAMPLES = 0, RT_CNT_SEGMENTS, RT_CNT_NODES, RT_CNT_SPHERES, RT_CNT_MSPHERES, RT_CNT_RECTS,
     RT_CNT_INSTANCED, RT_CNT_MEDIA, RT_CNT_SHADES, RT_CNT_NOISE, RT_CNT_N
 };
+// The rest of the stats buffer (uint64 slots after the RT_CNT_N counters): stage
+// cycles (RT_FLAG_PROFILE), wave-level trip counts (RT_FLAG_COUNT), the wave
+// timeline (RT_FLAG_PROFILE), the shading-stage material divergence (RT_FLAG_COUNT:
+// wave shade passes, distinct scatter materials summed over them, scattering lanes;
+// RT_FLAG_PROFILE: cycles in the material scatter branches).
+enum {
+    RT_STAT_PROF = RT_CNT_N, RT_STAT_WAVE = RT_CNT_N + 4, RT_STAT_TIME = RT_CNT_N + 9, RT_STAT_SHADE = RT_CNT_N + 16,
+    RT_STATS_LEN = RT_CNT_N + 20
+};

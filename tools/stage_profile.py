@@ -25,6 +25,9 @@ pr = out["profile"]
 tot = sum(pr[k] for k in ("cycles_claim", "cycles_traverse", "cycles_media", "cycles_shade"))
 shares = {k: pr[k] / tot for k in ("cycles_claim", "cycles_traverse", "cycles_media", "cycles_shade")}
 c = out["count"]
+scatter_share = pr["cycles_scatter"] / tot
+scatter_eff = c["lane_scatters"] / (64 * max(1, c["wave_shade_passes"]))
+kinds = c["wave_shade_kinds"] / max(1, c["wave_shade_passes"])
 print(json.dumps({"scene": scene_name, "image": [nx, ny], "spp": spp, "plain_kernel_ms": out["plain"]["kernel_ms"],
                   "profile_kernel_ms": pr["kernel_ms"], "stage_share": shares,
                   "per_ray": {k: c[k] / max(1, c["segments"]) for k in
@@ -39,5 +42,12 @@ print(json.dumps({"scene": scene_name, "image": [nx, ny], "spp": spp, "plain_ker
                       "sphere_draw_rounds": c["lane_sphere_draw_trips"] / (64 * max(1, c["wave_sphere_draw_trips"])),
                       "wave_node_steps_per_iteration": c["wave_node_trips"] / max(1, c["wave_iterations"]),
                       "wave_prim_steps_per_iteration": c["wave_prim_trips"] / max(1, c["wave_iterations"]),
-                      "wave_sphere_draw_rounds_per_iteration": c["wave_sphere_draw_trips"] / max(1, c["wave_iterations"])}},
+                      "wave_sphere_draw_rounds_per_iteration": c["wave_sphere_draw_trips"] / max(1, c["wave_iterations"]),
+                      "scatter_lanes": scatter_eff,
+                      "scatter_materials_per_pass": kinds},
+                  # material scatter branches (shade_finish, part of cycles_shade): their share of
+                  # the wave cycles, and what a free, perfect material sort could remove — every
+                  # pass one material with all 64 lanes scattering: share x (1 - efficiency / kinds)
+                  "scatter_share": scatter_share,
+                  "material_sort_bound": scatter_share * (1 - scatter_eff / max(1e-9, kinds))},
                  indent=1))
