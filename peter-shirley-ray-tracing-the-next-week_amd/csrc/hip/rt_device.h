@@ -136,7 +136,11 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t skey, uint32_t pixel, ui
 struct Rng {
     uint64_t x;      // the sample's drand48 state
     uint64_t mkey;   // medium stream key, derived once per sample
-    __device__ __forceinline__ void start(uint64_t k) { x = k & kLcgM; mkey = mix64(k ^ 0xD1B54A32D192ED03ull); }
+    // media = false: the scene has no constant_medium, so the medium key is never read
+    __device__ __forceinline__ void start(uint64_t k, bool media = true) {
+        x = k & kLcgM;
+        mkey = media ? mix64(k ^ 0xD1B54A32D192ED03ull) : 0;
+    }
     __device__ __forceinline__ double next() { x = lcg_step(x); return u48x(x); }
     __device__ __forceinline__ void skip() { x = lcg_step(x); }   // a draw whose value is not used
     __device__ __forceinline__ void skip2() { x = lcg_step(lcg_step(x)); }   // two of them (a constant jump's

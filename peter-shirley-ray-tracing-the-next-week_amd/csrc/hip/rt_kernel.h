@@ -20,7 +20,8 @@
 #define RT_FEAT_UV 2        // a material reads (u, v): image_texture
 #define RT_FEAT_CHECKER 4   // checker_texture
 #define RT_FEAT_PRESCAN 8   // BVH scene with pre-scanned primitives (RtKernelArgs.nprescan > 0)
-#define RT_FEAT_ALL 15
+#define RT_FEAT_MEDIA 16    // constant_medium (without it: no media stage, no medium-stream key per sample)
+#define RT_FEAT_ALL 31
 
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)

@@ -72,7 +72,7 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 // kFeat (RT_FEAT_*): the scene features the variant carries code for — instance
 // chains (cornell scenes), (u, v)-reading materials (earth()), checker textures
 // (the random scenes).  The host launches the smallest compiled variant covering
-// the scene (final(): none of them); RT_FEAT_ALL runs anything.
+// the scene (final(): media only); RT_FEAT_ALL runs anything.
 // kMode, the closest-hit search:
 //   0  BVH in HBM (nodes through L1/L2), 4-wave workgroups, 24-entry LDS stacks;
 //   1  BVH2 nodes in LDS (one workgroup of RT_LDS_BLOCK threads per CU copies them
@@ -82,7 +82,8 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 template <bool kCount, bool kProf, int kWidth, int kFeat, int kMode>
 __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
     constexpr bool kInst = (kFeat & RT_FEAT_INST) != 0, kUV = (kFeat & RT_FEAT_UV) != 0,
-                   kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0;
+                   kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0,
+                   kMedia = (kFeat & RT_FEAT_MEDIA) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
     __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : (kWidth >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH)][64];
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     uint64_t *pre_key = lds_pre_key[wave];
     float2 *pre_uv = lds_pre_uv[wave];
     // the media records are read from LDS (one broadcast read per medium)
-    load_media<kBlock>(A, lds_media);
+    if (kMedia) load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) {
         store_camera(A, lds_cam);
         lds_mconst.c02 = 0.2;
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     auto camera_begin = [&](bool starting, float &cu_, float &cv_) {
         if (starting) {
             if (pre_have) {   // a work item's first sample: made by refill
-                g.start(pre_k);
+                g.start(pre_k, kMedia);
                 g.skip2();   // the two jitter draws
                 cu_ = pre_cuv.x;
                 cv_ = pre_cuv.y;
@@ -298,7 +299,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 const uint32_t c = item / A.npix;
                 const uint32_t xy = A.job_xy[item - c * A.npix];
                 const int px = (int)(xy & 0xFFFFu), j = A.ny - 1 - (int)(xy >> 16);
-                g.start(sample_key(skey, (uint32_t)(j * A.nx + px), (uint32_t)s_cur + A.sample_offset));
+                g.start(sample_key(skey, (uint32_t)(j * A.nx + px), (uint32_t)s_cur + A.sample_offset), kMedia);
                 cu_ = div_rn((float)((double)px + g.next()), (float)A.nx, A.rnx);
                 cv_ = div_rn((float)((double)j + g.next()), (float)A.ny, A.rny);
             }
@@ -463,8 +464,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            const int med_mat = media_hit<kCount, kInst>(A, lds_media, (LdsMediaConsts *)&lds_mconst, r, rd, depth, g, have,
-                                                         best_t, cnt);
+            const int med_mat = kMedia ? media_hit<kCount, kInst>(A, lds_media, (LdsMediaConsts *)&lds_mconst, r, rd, depth, g,
+                                                                  have, best_t, cnt)
+                                       : -1;
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);
                 hr.n = mk(1, 0, 0);
@@ -653,8 +655,10 @@ static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipS
 template <int kLds>
 static hipError_t launch_features(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     switch (a->features) {
-    case 0: return launch_variant<2, 0, kLds>(a, grid, mode, stream);
+    case 0:
+    case RT_FEAT_MEDIA: return launch_variant<2, RT_FEAT_MEDIA, kLds>(a, grid, mode, stream);
     case RT_FEAT_INST: return launch_variant<2, RT_FEAT_INST, kLds>(a, grid, mode, stream);
+    case RT_FEAT_INST | RT_FEAT_MEDIA: return launch_variant<2, RT_FEAT_INST | RT_FEAT_MEDIA, kLds>(a, grid, mode, stream);
     case RT_FEAT_CHECKER:
     case RT_FEAT_CHECKER | RT_FEAT_PRESCAN:
         return launch_variant<2, RT_FEAT_CHECKER | RT_FEAT_PRESCAN, kLds>(a, grid, mode, stream);
@@ -662,9 +666,10 @@ static hipError_t launch_features(const RtKernelArgs *a, int grid, int mode, hip
     }
 }
 
-// Compiled variants: every feature (any scene), none (final()), instances only
-// (cornell_box, cornell_smoke), checker + pre-scan (the random scenes), each with the BVH2
-// in HBM or in LDS; the wide BVHs (4, 8, compressed 8) run the all-feature variant from HBM.
+// Compiled variants: every feature (any scene), media only (final(), and scenes with
+// no feature), instances (cornell_box), instances + media (cornell_smoke), checker +
+// pre-scan without media (the random scenes), each with the BVH2 in HBM or in LDS; the
+// wide BVHs (4, 8, compressed 8) run the all-feature variant from HBM.
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream) {
     if (a->scan) return launch_features<2>(a, grid, mode, stream);
     if (a->bvh_width == 4) return launch_variant<4, RT_FEAT_ALL, 0>(a, grid, mode, stream);
@@ -705,7 +710,8 @@ static int lds_static_of() {
     return (int)fa.sharedSizeBytes;
 }
 extern "C" int rt_megakernel_lds_static_actual(void) {
-    return std::max(std::max(lds_static_of<0>(), lds_static_of<RT_FEAT_INST>()),
+    return std::max(std::max(std::max(lds_static_of<RT_FEAT_MEDIA>(), lds_static_of<RT_FEAT_INST>()),
+                             lds_static_of<RT_FEAT_INST | RT_FEAT_MEDIA>()),
                     std::max(lds_static_of<RT_FEAT_CHECKER | RT_FEAT_PRESCAN>(), lds_static_of<RT_FEAT_ALL>()));
 }
 

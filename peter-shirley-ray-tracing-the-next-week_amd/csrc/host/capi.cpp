@@ -709,7 +709,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
-                 (s->has_checker ? RT_FEAT_CHECKER : 0) | (s->nprescan > 0 ? RT_FEAT_PRESCAN : 0);
+                 (s->has_checker ? RT_FEAT_CHECKER : 0) | (s->nprescan > 0 ? RT_FEAT_PRESCAN : 0) |
+                 (s->nmedia > 0 ? RT_FEAT_MEDIA : 0);
     // RTNW_FEAT_ALL=1 runs the all-feature variant (the one the wide BVHs use): A/B runs only
     if (const char *e = std::getenv("RTNW_FEAT_ALL")) if (std::atoi(e)) a.features = RT_FEAT_ALL;
     for (int k = 0; k < 3; k++) {

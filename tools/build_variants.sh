@@ -25,6 +25,6 @@ done
 rc=0
 for i in "${!pids[@]}"; do
   wait "${pids[$i]}" || { echo "variant ${names[$i]} failed"; rc=1; }
-  grep -A8 "ILb0ELb0ELi2ELi0ELi1E" ../variants/${names[$i]}/resource.txt | grep -E "VGPRs:|Scratch" | sed "s/.*remark: */${names[$i]}: /"
+  grep -A8 "ILb0ELb0ELi2ELi16ELi1E" ../variants/${names[$i]}/resource.txt | grep -E "VGPRs:|Scratch" | sed "s/.*remark: */${names[$i]}: /"
 done
 exit $rc

@@ -41,8 +41,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "peter-shirley-ray-tracing-the-next-week_amd")
 # the timed variant per config: <count, profile, width, features, mode>
 SYMBOLS = {
-    "c4": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi0ELi1EEEv12RtKernelArgs",    # final(): no features, LDS BVH2
-    "c5": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi0ELi1EEEv12RtKernelArgs",
+    "c4": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi16ELi1EEEv12RtKernelArgs",   # final(): media only, LDS BVH2
+    "c5": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi16ELi1EEEv12RtKernelArgs",
     "c3": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi12ELi1EEEv12RtKernelArgs",   # random_motion: checker + pre-scan
     "c2": "_ZN12_GLOBAL__N_113rt_megakernelILb0ELb0ELi2ELi1ELi2EEEv12RtKernelArgs",    # cornell_box: instances, flat scan
 }
