@@ -420,3 +420,44 @@ def test_bvh_widths_agree_bitwise(monkeypatch, scene, nx, ny, ns):
     ref = out["2", "0", "0"].view(np.uint32)
     for k, img in out.items():
         assert np.array_equal(img.view(np.uint32), ref), k
+
+
+@pytest.mark.parametrize("scene,nx,ny,ns", [("final", 40, 40, 8), ("cornell_box", 32, 32, 8),
+                                            ("cornell_smoke", 32, 32, 8), ("random_motion", 40, 20, 8),
+                                            ("simple_light", 32, 16, 8)])
+def test_feature_variants_match_the_all_feature_kernel(monkeypatch, scene, nx, ny, ns):
+    """The host launches the smallest megakernel variant covering the scene's features
+    (RT_FEAT_*: final() media only, cornell_box instances, cornell_smoke instances +
+    media, the random scenes checker + pre-scan without media, simple_light none): its
+    image must be the all-feature kernel's (RTNW_FEAT_ALL=1) bit for bit — a variant
+    only drops code the scene cannot reach (a scene without media derives no
+    medium-stream key, constant_medium.h:36's draws never happen)."""
+    cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene]
+    cam = rtnw.Camera.preset(cam_name, nx, ny)
+    p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, seed=21)
+    sc = rtnw.Scene.builtin(scene)
+    small = sc.render_tile(cam, p, 0, 0, nx, ny)
+    monkeypatch.setenv("RTNW_FEAT_ALL", "1")
+    full = sc.render_tile(cam, p, 0, 0, nx, ny)
+    assert np.array_equal(small.view(np.uint32), full.view(np.uint32))
+
+
+@pytest.mark.parametrize("scene,one_material", [("cornell_box", True), ("final", False)])
+def test_shade_divergence_counters(scene, one_material):
+    """RT_FLAG_COUNT's material-divergence counters (lane convergence):
+    cornell_box scatters only lambertian surfaces (its light ends paths), so every wave
+    pass through the scatter branches runs exactly one material; final() mixes
+    lambertian, metal, dielectric and isotropic, so a pass runs between 1 and 4.  A
+    scattering lane is a shading lane, and a pass holds at most 64 of them."""
+    nx, ny, ns = 48, 48, 16
+    cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene]
+    cam = rtnw.Camera.preset(cam_name, nx, ny)
+    p = rtnw.RenderParams(nx, ny, ns, max_depth=depth, background=bg, seed=5, flags=rtnw.RT_FLAG_COUNT)
+    _, st = rtnw.Scene.builtin(scene).render_tile(cam, p, 0, 0, nx, ny, stats=True)
+    passes, kinds, lanes = st["wave_shade_passes"], st["wave_shade_kinds"], st["lane_scatters"]
+    assert 0 < passes <= st["wave_iterations"]
+    assert 0 < lanes <= min(st["shades"], 64 * passes)
+    if one_material:
+        assert kinds == passes
+    else:
+        assert passes < kinds <= 4 * passes
