@@ -306,6 +306,9 @@ def main():
     ap.add_argument("--dump", default="", help="rank 0 saves the last step's float image (.npy) here")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo rehearses several ranks on one GPU")
+    ap.add_argument("--share-of", type=int, default=0,
+                    help="profiling: one process renders rank 0's share of config 5 split over N ranks "
+                         "(the PMC profile key c5_nN that an N-GPU run's roofline reads)")
     ap.add_argument("--gather", default="auto", choices=["auto", "torch", "native"],
                     help="the C ABI's rt_dist_gather (ncclGather on its own RCCL comm; auto with nccl), or "
                          "torch.distributed.gather (auto with gloo)")
@@ -340,13 +343,16 @@ def main():
         sys.exit(2)
     dev = torch.device("cuda", gpu)
 
-    cfg = args.config or ("c4" if world == 1 else "c5")
+    share = args.share_of if world == 1 and args.share_of > 1 else 0
+    cfg = "c5" if share else (args.config or ("c4" if world == 1 else "c5"))
     scene_name, w1, h1, spp, scaling = CONFIGS[cfg]
     spp = args.spp or spp
     cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
     nx, ny = (w1, h1) if scaling == "strong" else image_for(world, w1, h1)
     if world > 1:
         all_tiles = [rtnw.pixels_for_rank(nx, ny, r, world) for r in range(world)]
+    elif share:   # a rank's share alone (profiling; its image is that share's pixels)
+        all_tiles = [rtnw.pixels_for_rank(nx, ny, 0, share)]
     else:
         all_tiles = [[(0, 0, nx, ny)]]
     all_counts = [int(np.asarray(t).reshape(-1, 4)[:, 2:].prod(axis=1).sum()) * 3 for t in all_tiles]
@@ -381,7 +387,8 @@ def main():
 
     workload = f"{cfg}: {scene_name}() {nx}x{ny} pixels x {spp} spp, depth {depth}" + \
         (f", split over {world} GPUs" if world > 1 and scaling == "strong" else
-         (f", {world} GPUs x {nx * ny // world} pixels" if world > 1 else ""))
+         (f", {world} GPUs x {nx * ny // world} pixels" if world > 1 else "")) + \
+        (f", rank 0's share of {share} (profiling)" if share else "")
     for i in range(args.warmup):
         st = step()
         log(f"[rank {rank}] warmup {i}: kernel {st['kernel_ms']:.1f} ms")
@@ -405,7 +412,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    samples_per_step = nx * ny * spp
+    samples_per_step = nx * ny * spp if not share else all_counts[0] // 3 * spp
     value = samples_per_step * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -420,7 +427,11 @@ def main():
     # the PMC profile of this config (c5 on several GPUs: c4's, whose per-sample wave
     # coherence is the closer one — an interleaved rank's 8x8 work block spans 32x16
     # pixels of the 1000^2 view, against 8x8 of c4's 500^2 and 8x8 of c5's on one GPU)
-    prof = read_profile(cfg, sha) or (read_profile("c4", sha) if cfg == "c5" and world > 1 else None)
+    # the PMC profile of this config; c5 on N GPUs: the profile of one rank's share
+    # (bench.py --share-of N on one GPU, key c5_nN: an interleaved rank's work blocks
+    # span a4 x 8b pixels of the view, so its coherence is its own)
+    nshare = world if world > 1 else share
+    prof = read_profile(f"c5_n{nshare}" if cfg == "c5" and nshare > 1 else cfg, sha)
     roof = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G wave-VALU-instr/s",
             "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
             "frac_uniform_2cyc": None, "valu_issue_cycles_per_instr": None,
@@ -479,7 +490,7 @@ def main():
             roof["traffic"] = tr
             roof["hbm_frac"] = tr / avg_kernel_s / (HBM_PEAK_GBS * 1e9)
 
-    if rank == 0 and (args.ppm or args.dump):
+    if rank == 0 and (args.ppm or args.dump) and not share:
         if world == 1:
             img = out[: nx * ny * 3].cpu().numpy().reshape(ny, nx, 3)
         else:   # the last timed step's gathered shares, unpacked on the root
@@ -518,9 +529,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": None,
         }
-        if world == 1:
+        if world == 1 and not share:
             res["end_to_end"] = end_to_end(scene_name, cam, params, nx, ny, dev)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not share and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(scene_name, w1, h1)
         print(json.dumps(res), flush=True)
     if comm is not None:

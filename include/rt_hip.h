@@ -207,7 +207,8 @@ typedef struct rt_stats {
     double stack_depth;           /* traversal stack entries per lane (LDS variants: the BVH depth + 1) */
     double scan_groups;           /* flat scan instead of a BVH (<= 64 primitives): its instance groups, else 0 */
     double prescan;               /* BVH scenes: largest primitives kept out of the BVH, tested first in lockstep */
-    double wave_exhaust_first_us; /* RT_FLAG_PROFILE wave timeline (s_memrealtime, us after the first wave started):
+    double wave_exhaust_first_us; /* RT_FLAG_PROFILE wave timeline of the job's last launch (s_memrealtime, us
+                                     after its first wave started):
                                      the first wave to find the work pool empty */
     double wave_exhaust_last_us;  /*   the last wave to find it empty */
     double wave_end_first_us;     /*   the first wave to finish */

@@ -57,6 +57,16 @@ namespace {
 #define RT_DESCEND_STEPS 2
 #endif
 
+// Cooperative leaf tests in the LDS-BVH variant (rt_device.h coop_leaves); 0: each
+// lane tests its own parked leaf (A/B)
+#ifndef RT_COOP_LEAF
+#define RT_COOP_LEAF 0
+#endif
+// ... with a second parked leaf per lane (descend<kPark2>)
+#ifndef RT_COOP_PARK2
+#define RT_COOP_PARK2 0
+#endif
+
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
@@ -85,6 +95,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0,
                    kMedia = (kFeat & RT_FEAT_MEDIA) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
+    // the LDS-BVH2 variant tests its parked leaves with the whole wave (coop_leaves)
+    constexpr bool kCoopLeaf = RT_COOP_LEAF && kLds && kWidth == 2 && RT_LDS_SIGNED;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
     __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : (kWidth >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH)][64];
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
@@ -406,7 +418,20 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             for (;;) {
                 if (wballot(phase == PH_TRAV) == 0ull) break;
                 if (__popcll(wballot(phase == PH_READY)) >= RT_READY_BATCH) break;
-                if (phase == PH_TRAV) {
+                if constexpr (kCoopLeaf) {
+                    // descend, then the parked leaves tested by the whole wave (coop_leaves)
+                    const bool trav = phase == PH_TRAV;
+                    uint32_t pleaf = RT_EMPTY_CHILD, pleaf2 = RT_EMPTY_CHILD;
+                    if (trav) {
+                        Slab sl = make_slab(r, A.tmin);
+                        lnodes.prepare(sl);
+                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS, RT_COOP_PARK2>(lnodes, node, sl, best_t,
+                                                                                                  stk, sp, cnt, &pleaf2);
+                    }
+                    coop_leaves<kCount, kInst, RT_COOP_PARK2>(pleaf, pleaf2, r, A.prims, A.insts, A.tmin, slots, lane,
+                                                              best_t, best_key, best_prim, cnt);
+                    if (trav && node == RT_EMPTY_CHILD) phase = PH_READY;   // stack empty too (popped above)
+                } else if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
                     Slab sl = make_slab(r, A.tmin);
                     uint32_t pleaf;
@@ -415,6 +440,13 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                         pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt);
                     else
                         pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt);
+                    if (kCount && RT_COOP_STATS) {   // experiment: leaf rounds and their primitives
+                        const uint64_t own = wballot(pleaf != RT_EMPTY_CHILD);
+                        const uint32_t n = pleaf != RT_EMPTY_CHILD ? RT_LEAF_COUNT(pleaf) : 0u;
+                        uint32_t sum = 0;
+                        for (int b = 0; b < 4; ++b) sum += (uint32_t)__popcll(wballot((n >> b) & 1u)) << b;
+                        if (own && first_active()) { cnt.w_rius++; cnt.l_rius += sum; }
+                    }
                     if (pleaf != RT_EMPTY_CHILD) {
                         const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
                         // primitives in pairs: both 32-B heads are fetched before either test
@@ -550,7 +582,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         atomicMax(&T[2], (unsigned long long)(rt_exhaust ? rt_exhaust : rt_end));
         atomicMax(&T[3], ~rt_end);
         atomicMax(&T[4], rt_end);
-        atomicAdd(&T[5], rt_end - (unsigned long long)rt_start);
+        atomicAdd(&T[5], rt_end);   // sum of the waves' ends: their mean, on the same clock as T[0..4]
         atomicAdd(&T[6], 1ull);
         if (A.wave_log) {   // HW_ID (cu, simd, wave slot, se) and XCC_ID through s_getreg (reads)
             const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);

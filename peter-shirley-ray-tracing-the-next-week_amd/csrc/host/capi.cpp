@@ -409,6 +409,12 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
                 groups.push_back(g);
             }
             rt_dgroup &g = groups.back();
+            // scan_group (rt_device.h) walks a group's runs in the enum order of the kinds,
+            // from 8-bit counts packed at 8 * kind in `kinds` (yz rects in nyz)
+            static_assert(RT_PRIM_SPHERE == 0 && RT_PRIM_MOVING_SPHERE == 1 && RT_PRIM_XY_RECT == 2 &&
+                              RT_PRIM_XZ_RECT == 3 && RT_PRIM_YZ_RECT == 4,
+                          "rt_dgroup.kinds packs the primitive kinds 0..3 by their enum value");
+            static_assert(RT_SCAN_MAX < 256, "rt_dgroup.kinds holds 8-bit counts");
             g.count++;
             if (pr.kind == RT_PRIM_YZ_RECT) g.nyz++;
             else g.kinds += 1 << (8 * pr.kind);     // count <= RT_SCAN_MAX < 256 per kind
@@ -416,6 +422,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             g.bx[2] = std::min(g.bx[2], lo[1]); g.bx[3] = std::max(g.bx[3], hi[1]);
             g.bz[0] = std::min(g.bz[0], lo[2]); g.bz[1] = std::max(g.bz[1], hi[2]);
         }
+    }
+    for (const rt_dgroup &g : groups) {   // the per-kind runs cover the group exactly
+        const int runs = (g.kinds & 0xff) + ((g.kinds >> 8) & 0xff) + ((g.kinds >> 16) & 0xff) +
+                         ((g.kinds >> 24) & 0xff) + g.nyz;
+        if (runs != g.count) return cleanup(fail(RT_ERR_INVALID, "flat scan: a group's kind counts do not add up"));
     }
     std::vector<rt_dprim> prims(d->nprims), bprims(d->nboundary);
     for (int i = 0; i < d->nprims; i++) {
@@ -559,8 +570,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             lds_cu = 0;
         const long stat = std::max<long>(rt_megakernel_lds_static_bytes(), rt_megakernel_lds_static_actual());
         const long need_actual = need - rt_megakernel_lds_static_bytes() + stat;
+        // (its cooperative leaf tests pack the list-order key and the primitive index
+        // into 16 bits each, rt_device.h pack_hit: fewer than RT_COOP_MAX_PRIMS primitives)
         s->lds_nodes = want && !s->scan && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
-                       s->nnodes <= RT_LDS_NODE_CAP && need_actual <= std::min<long>(RT_LDS_BUDGET, lds_cu);
+                       s->nnodes <= RT_LDS_NODE_CAP && d->nprims < RT_COOP_MAX_PRIMS &&
+                       need_actual <= std::min<long>(RT_LDS_BUDGET, lds_cu);
         if (s->lds_nodes)
             for (int mode = 0; mode < 3; mode++) s->grid[mode] = s->cus;
     }
@@ -744,6 +758,10 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     // items claimed) per wave and batch (tools/tail_probe.py --wave-log; diagnostics)
     const char *wave_log_path = prof ? std::getenv("RTNW_WAVE_LOG") : nullptr;
     unsigned long long *wave_log = nullptr;
+    struct FreeOnExit {   // every return below, error paths included, frees the log buffer
+        unsigned long long *&p;
+        ~FreeOnExit() { if (p) (void)hipFree(p); }
+    } wave_log_guard{wave_log};
     const size_t wave_log_n = (size_t)s->grid[2] * ((s->lds_nodes ? RT_LDS_BLOCK : RT_BLOCK) / 64) * 5;
     if (wave_log_path) {
         HIP_TRY(hipMalloc(&wave_log, wave_log_n * sizeof(unsigned long long)));
@@ -784,6 +802,9 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         const int rmode = (b == 0 ? RT_RESOLVE_FIRST : 0) | (b + 1 == nbatches ? RT_RESOLVE_LAST : 0) |
                           (sum_in ? RT_RESOLVE_SUM_IN : 0) | (sum_out ? RT_RESOLVE_RAW : 0);
         HIP_TRY(hipMemsetAsync(s->counter, 0, 64, stream));
+        // the wave timeline describes the last batch: its slots start from zero each launch
+        if (prof)
+            HIP_TRY(hipMemsetAsync((unsigned long long *)s->stats + RT_STAT_TIME, 0, 7 * sizeof(unsigned long long), stream));
         HIP_TRY(hipEventRecord(s->ev[0], stream));
         HIP_TRY(rt_launch_megakernel(&a, s->grid[mode], mode, stream));
         HIP_TRY(hipEventRecord(s->ev[1], stream));
@@ -809,7 +830,6 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         }
     }
 
-    if (wave_log) (void)hipFree(wave_log);
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         stats->samples = (double)s->npix * (double)p->spp;
@@ -859,7 +879,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->wave_exhaust_last_us = ((double)T[2] - t0) * us;
             stats->wave_end_first_us = ((double)~T[3] - t0) * us;
             stats->wave_end_last_us = ((double)T[4] - t0) * us;
-            stats->wave_end_mean_us = T[6] ? (double)T[5] / (double)T[6] * us : 0.0;
+            stats->wave_end_mean_us = T[6] ? ((double)T[5] / (double)T[6] - t0) * us : 0.0;   // T[5]: sum of ends
         }
         stats->grid = (double)s->grid[mode];
         stats->lds_level = s->lds_nodes ? 1.0 : 0.0;
@@ -960,7 +980,10 @@ int rt_checkpoint_read(const char *path, rt_checkpoint *hdr, float *sums, uint64
     if (std::fread(&h, sizeof h, 1, f) != 1 || h.magic != RT_CHECKPOINT_MAGIC || h.version != RT_CHECKPOINT_VERSION) {
         rc = fail(RT_ERR_INVALID, std::string("not a checkpoint: ") + path);
     } else if (h.nx <= 0 || h.ny <= 0 || h.count % 3 != 0 || h.count > 3ull * (uint64_t)h.nx * (uint64_t)h.ny ||
-               fsize < 0 || (uint64_t)fsize != sizeof h + h.count * sizeof(float) + sizeof(uint64_t)) {
+               fsize < (long)(sizeof h + sizeof(uint64_t)) ||
+               // the payload's size by division: count * 4 would wrap for a crafted count
+               ((uint64_t)fsize - sizeof h - sizeof(uint64_t)) % sizeof(float) != 0 ||
+               ((uint64_t)fsize - sizeof h - sizeof(uint64_t)) / sizeof(float) != h.count) {
         rc = fail(RT_ERR_INVALID, std::string("corrupt checkpoint header (count / image size / file size): ") + path);
     } else if (sums) {   // sums == NULL: header only (to size the buffer)
         if (h.count > cap) {

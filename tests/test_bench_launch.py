@@ -2,8 +2,8 @@
 launcher around it starts the N rank processes itself (bench.launch_ranks), a
 `--gpus` that disagrees with a launcher's WORLD_SIZE is refused, a rank that dies
 takes the job down instead of leaving its peers in the rendezvous, and (GPU) the
-2-rank job renders config 5's workload whose gathered image is bitwise the 1-GPU
-image (the RNG is keyed by pixel and sample)."""
+2- and 8-rank jobs render config 5's workload whose gathered image is bitwise the
+1-GPU image (the RNG is keyed by pixel and sample)."""
 import json
 import os
 import subprocess
@@ -51,24 +51,28 @@ def test_rccl_refuses_more_ranks_than_gpus():
 
 
 @pytest.mark.gpu
-def test_two_rank_self_launched_bench_gathers_the_one_gpu_image(tmp_path):
-    """The driver's N-GPU command shape, rehearsed on one GPU with gloo: 2 ranks,
-    config 5's image (final() 1000 x 1000) at 8 spp, strong scaling; the gathered
-    image equals a 1-GPU render of the same job bit for bit."""
-    dump = str(tmp_path / "c5_2ranks.npy")
-    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-backend", "gloo", "--spp", "8", "--steps", "1",
-                        "--warmup", "0", "--no-cpu-baseline", "--dump", dump],
-                       env=_env(), capture_output=True, text=True, timeout=300)
+@pytest.mark.parametrize("n,spp", [(2, 8), (8, 2)])
+def test_self_launched_bench_gathers_the_one_gpu_image(tmp_path, n, spp):
+    """The driver's N-GPU command shape, rehearsed on one GPU with gloo: N ranks
+    (2 = 2x1, 8 = the 4x2 pixel interleave the 8-GPU node runs), config 5's image
+    (final() 1000 x 1000), strong scaling, through bench.py's own launcher, its gather
+    and rank 0's unpack; the gathered image equals a 1-GPU render of the same job bit
+    for bit."""
+    dump = str(tmp_path / f"c5_{n}ranks.npy")
+    p = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dist-backend", "gloo", "--spp", str(spp),
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--dump", dump],
+                       env=_env(), capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["n_gpus"] == n and line["scaling"] == "strong"
     assert line["config"]["workload"].startswith("c5: final() 1000x1000")
-    assert line["config"]["image"] == [1000, 1000] and line["config"]["spp"] == 8
+    assert line["config"]["image"] == [1000, 1000] and line["config"]["spp"] == spp
+    assert line["config"]["rank_layout"] == "pixel interleave %dx%d" % {2: (2, 1), 8: (4, 2)}[n]
     img = np.load(dump)
 
     import rtnw
     sc = rtnw.Scene.builtin("final", device=0)
     cam = rtnw.Camera.preset("cornell", 1000, 1000)
-    one = sc.render_tile(cam, rtnw.RenderParams(1000, 1000, 8, max_depth=50, seed=2024), 0, 0, 1000, 1000)
+    one = sc.render_tile(cam, rtnw.RenderParams(1000, 1000, spp, max_depth=50, seed=2024), 0, 0, 1000, 1000)
     sc.close()
     assert np.array_equal(img.view(np.uint32), one.view(np.uint32))

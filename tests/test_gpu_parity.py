@@ -22,6 +22,18 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 TOL_RMS = 1e-3
+# Bit-exact fraction of the framebuffer floats against the oracle.  What differs
+# is ocml vs glibc sinf / log / pow last bits, which now and then send one sample
+# down another path; a pixel is bit-exact only if ALL its samples are, so the bar is
+# per sample: at most 1 in 2,000 samples may differ (measured: 1 in 2,800 at 8 spp,
+# smoke 0.9971; 1 in 6,300 at 1000 spp, the c4 centre crop 0.854 = 55 of 64 pixels).
+# Capped at 0.99 of the pixels, so a low-spp case that breaks more than 1 % of the
+# pixels' bits fails.
+EXACT_PER_SAMPLE = 0.9995
+
+
+def exact_min(spp):
+    return min(0.99, EXACT_PER_SAMPLE ** spp)
 THREADS = min(16, os.cpu_count() or 1)
 
 
@@ -82,7 +94,7 @@ def test_gpu_matches_oracle(scene, nx, ny, ns, chunk, seed):
     exact = np.mean(g.view(np.uint32) == o.view(np.uint32))
     print(f"{scene}: gamma RMS {rms}, bit-exact fraction {exact:.4f}")
     assert (rms <= TOL_RMS).all(), rms
-    assert exact > 0.5
+    assert exact >= exact_min(ns), exact
 
 
 EDGE_PARAMS = [   # (scene, nx, ny, spp, chunk, max_depth, background, t_min)
@@ -351,7 +363,7 @@ def test_baseline_configs_at_full_spp_against_oracle_crops(scene, nx, ny, ns):
         exact.append(float(np.mean(crop.view(np.uint32) == o.view(np.uint32))))
         assert (rms <= TOL_RMS).all(), (x0, y0, rms)
     print(f"{scene} {nx}x{ny}x{ns}: crops bit-exact fractions {exact}")
-    assert min(exact) > 0.5, exact
+    assert min(exact) >= exact_min(ns), exact
 
 
 @pytest.mark.parametrize("claim,tail", [("1", "0"), ("3", "2"), ("16", "0"), ("16", "1"), ("8", "50")])
@@ -373,6 +385,7 @@ def test_medium_size_final_parity():
     exact = np.mean(g.view(np.uint32) == o.view(np.uint32))
     print(f"final 100x100x32: gamma RMS {rms} bit-exact {exact:.4f}")
     assert (rms <= TOL_RMS).all()
+    assert exact >= exact_min(32), exact
 
 
 def test_ppm_from_gpu_mean_matches_oracle_quantiser():

@@ -241,6 +241,19 @@ def test_checkpoint_round_trip_and_corruption(tmp_path):
         (tmp_path / "d.rtck").write_bytes(bytes(raw))
         with pytest.raises(rtnw.RtError, match="corrupt checkpoint header"):
             rtnw.read_checkpoint(str(tmp_path / "d.rtck"))
+    # a count whose byte size wraps 64 bits: 2^62 + 602 (divisible by 3, within
+    # 3 nx ny for a 2^31 - 1 square image) times 4 is 2408 mod 2^64, the size of 602
+    # floats, so a multiply-based size check would pass it; the header-only read
+    # (the one that sizes the caller's buffer) must refuse it too
+    raw = bytearray(path.read_bytes())
+    payload_end = len(raw) - 8
+    raw[payload_end:payload_end] = bytes(8)   # 600 -> 602 floats of payload
+    raw[off:off + 8] = ((1 << 62) + 602).to_bytes(8, "little")
+    for f in (rtnw.RtCheckpoint.nx, rtnw.RtCheckpoint.ny):
+        raw[f.offset:f.offset + 4] = (2 ** 31 - 1).to_bytes(4, "little")
+    (tmp_path / "e.rtck").write_bytes(bytes(raw))
+    with pytest.raises(rtnw.RtError, match="corrupt checkpoint header"):
+        rtnw.read_checkpoint(str(tmp_path / "e.rtck"))   # refused by its header-only call
 
 
 def test_shared_reciprocal_division_is_ieee(tmp_path):
