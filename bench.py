@@ -225,6 +225,24 @@ def read_profile(workload_key, sha=None):
     return (same or found)[-1]
 
 
+def read_lanes(workload_key, sha):
+    """VALU lane utilisation (SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)) of this
+    workload from the committed rocprofv3 pass of these very kernels
+    (profiles/r<NN>/lanes.json, tools/lanes_summary.py, matched by kernel_sha16), or
+    None when no pass of this build is committed."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "**", "lanes.json"), recursive=True),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        c = t.get("configs", {}).get(workload_key)
+        if sha and t.get("kernel_sha16") == sha and c and c.get("lane_utilisation"):
+            return c["lane_utilisation"], os.path.relpath(path, ROOT)
+    return None
+
+
 def end_to_end(scene_name, cam, params, nx, ny, dev):
     """SURVEY §8d's second reading of the metric: one more render of the same
     workload timed from scene creation (flatten, SAH build, upload to HBM) through
@@ -435,6 +453,7 @@ def main():
     roof = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G wave-VALU-instr/s",
             "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
             "frac_uniform_2cyc": None, "valu_issue_cycles_per_instr": None,
+            "lane_utilisation": None, "useful_frac": None, "useful_frac_uniform_2cyc": None, "lane_profile": None,
             "lds_level": int(st["lds_level"]), "stack_depth": int(st["stack_depth"]), "scan_groups": int(st["scan_groups"]), "prescan": int(st["prescan"]),
             "batches_per_step": int(st["batches"]),
             "valu_insts_per_sample": None, "profile": None, "profile_matches_library": None,
@@ -485,6 +504,16 @@ def main():
                 roof["valu_issue_cycles_per_instr"] = cpi
                 roof["peak"] = peak / 1e9
                 roof["frac"] = vi / avg_kernel_s / peak
+        # the share of the issued VALU slots' 64 lanes doing work (committed PMC pass of
+        # this build): frac says how full the issue roof is, useful_frac how much of it
+        # computes for a lane (the headroom is idle lanes, not issue)
+        lanes = read_lanes(f"c5_n{nshare}" if cfg == "c5" and nshare > 1 else cfg, sha)
+        if lanes:
+            roof["lane_utilisation"], roof["lane_profile"] = lanes
+            if roof["frac"] is not None:
+                roof["useful_frac"] = roof["frac"] * lanes[0]
+            if roof["frac_uniform_2cyc"] is not None:
+                roof["useful_frac_uniform_2cyc"] = roof["frac_uniform_2cyc"] * lanes[0]
         if prof.get("hbm_bytes_per_sample"):
             tr = prof["hbm_bytes_per_sample"] * rank_samples
             roof["traffic"] = tr

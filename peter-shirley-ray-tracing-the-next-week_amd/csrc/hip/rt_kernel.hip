@@ -89,8 +89,29 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 //      at launch; node steps read them with ds_read_b128), stacks of the scene's depth;
 //   2  flat scan of the primitive groups (rt_layout.h rt_dgroup), primitives in LDS,
 //      no BVH and no stack: scenes of at most RT_SCAN_MAX primitives.
+// Kernel arguments re-read each loop iteration (RT_KARGS_RELOAD): the persistent
+// loop reads ~40 uniform arguments; held in SGPRs across it they overflowed the 102
+// addressable SGPRs, which the compiler spilled into the lanes of a VGPR (v_writelane
+// at entry, a v_readlane — a VALU issue — per use).  Through a kernarg pointer that is
+// made opaque at the top of every iteration they are scalar loads (SMEM, scalar
+// cache) at their first use in the iteration instead (c4 53.01 -> 52.24 ms, c3
+// 45.55 -> 45.44 ms; SGPR spills 36 -> 0).
+#ifndef RT_KARGS_RELOAD
+#define RT_KARGS_RELOAD 1
+#endif
+typedef __attribute__((address_space(4))) const RtKernelArgs KArgs;
+__device__ __forceinline__ KArgs *opaque_kargs(KArgs *p) {
+#if RT_KARGS_RELOAD
+    asm volatile("" : "+s"(p));
+#endif
+    return p;
+}
+
 template <bool kCount, bool kProf, int kWidth, int kFeat, int kMode>
-__global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A) {
+__global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A_param) {
+    (void)A_param;   // read through ka (the same bytes: the kernarg segment holds A_param at offset 0)
+    KArgs *ka = (KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+#define A (*(const RtKernelArgs *)ka)
     constexpr bool kInst = (kFeat & RT_FEAT_INST) != 0, kUV = (kFeat & RT_FEAT_UV) != 0,
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0,
                    kMedia = (kFeat & RT_FEAT_MEDIA) != 0;
@@ -350,6 +371,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     };
 
     for (;;) {
+        // (not in the flat-scan variant: its scan reads the group records right at the
+        // iteration's start, and the reload measured slower there, c2 37.63 -> 37.88 ms)
+        if (!kScan) ka = opaque_kargs(ka);
         // ---- 1. claims and camera samples for lanes without a path --------------
         // (the first iteration, and paths that ended after the shading stage's
         // cooperative rounds: a metal's absorbed reflection; the others start their
@@ -614,6 +638,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
     }
 }
+
+#undef A
 
 // Adds one sample batch's partial sums to each pixel's running sum, in sample
 // order (main.cpp:311 `col += temp`, one add per sample with one sample per work

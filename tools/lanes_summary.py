@@ -32,6 +32,13 @@ def main():
     out = sys.argv[1]
     res = {"method": "SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU), first dispatch of the timed megakernel",
            "configs": {}}
+    # the device code object the passes ran (bench.py matches a profile to its library by it)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    try:
+        import bench
+        res["kernel_sha16"] = bench.kernel_sha16(os.environ.get("RTNW_LIB") or None)
+    except Exception as e:   # noqa: BLE001 (diagnostic tool: record why)
+        res["kernel_sha16_error"] = repr(e)
     for d in sorted(glob.glob(os.path.join(out, "lanes_c*"))):
         csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if not csvs:
