@@ -130,7 +130,8 @@ def lib():
         L.oracle_perlin_tables.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_drand48.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
         L.oracle_counter_draws.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
-        L.oracle_medium_draw.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+        L.oracle_medium_draw.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int]
         L.oracle_medium_draw.restype = ctypes.c_double
         L.oracle_scene_dump.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_long]
         L.oracle_set_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -230,8 +231,9 @@ def counter_draws(seed: int, pixel: int, sample: int, n: int) -> np.ndarray:
     return out
 
 
-def medium_draw(seed: int, pixel: int, sample: int, bounce: int, medium: int) -> float:
-    return lib().oracle_medium_draw(seed, pixel, sample, bounce, medium)
+def medium_draw(seed: int, pixel: int, sample: int, bounce: int, medium: int, nmedia: int) -> float:
+    """constant_medium draw of medium `medium` at segment `bounce` in a scene of `nmedia` media."""
+    return lib().oracle_medium_draw(seed, pixel, sample, bounce, medium, nmedia)
 
 
 def scene_dump(scene: str) -> str:

@@ -44,24 +44,26 @@ static uint64_t g_key = 0;        // counter mode: per-sample stream key
 static uint64_t g_x = 0;          // counter mode: the sample's drand48 state (restarted at key mod 2^48)
 static int g_med_ctx = -1;        // >=0 while a constant_medium (ordinal k) is being hit
 static int g_bounce = 0;          // top-level world->hit calls in this sample
+static int g_nmedia = 0;          // constant_media in the scene (tag_media's count)
 
 static inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-static const uint64_t kGamma = 0x9E3779B97F4A7C15ull;
 static inline uint64_t sample_key(uint64_t seed, uint32_t pixel, uint32_t sample) {
     return mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) ^ (((uint64_t)pixel << 32) | sample));
 }
-static inline double u48(uint64_t z) { return (double)(z >> 16) * 0x1p-48; }
 
 extern "C" double drand48(void) noexcept {
     if (g_mode == 0) return erand48(g_canon_state);
     if (g_med_ctx >= 0) {
-        uint64_t mk = mix64(g_key ^ 0xD1B54A32D192ED03ull);
-        uint64_t m = ((uint64_t)g_bounce << 8) | (uint64_t)g_med_ctx;
-        return u48(mix64(mk + (m + 1) * kGamma));
+        // the medium stream: drand48's generator from mix64(key ^ ..) mod 2^48, stepped
+        // once per medium and segment; this draw is its (bounce * nmedia + k + 1)-th value
+        uint64_t x = mix64(g_key ^ 0xD1B54A32D192ED03ull) & 0xFFFFFFFFFFFFull;
+        const uint64_t n = (uint64_t)g_bounce * (uint64_t)g_nmedia + (uint64_t)g_med_ctx + 1;
+        for (uint64_t i = 0; i < n; i++) x = (0x5DEECE66Dull * x + 0xBull) & 0xFFFFFFFFFFFFull;
+        return (double)x * 0x1p-48;
     }
     // drand48's own step on the sample's state (x = a x + c mod 2^48, x / 2^48)
     g_x = (0x5DEECE66Dull * g_x + 0xBull) & 0xFFFFFFFFFFFFull;
@@ -409,7 +411,7 @@ int main(int argc, char **argv) {
 
     bounce_counter *counted = nullptr;
     if (rng == "counter") {
-        int next = 0; tag_media(&world, next);
+        int next = 0; tag_media(&world, next); g_nmedia = next;
         counted = new bounce_counter(world);
         world = counted;
         g_mode = 1;

@@ -56,7 +56,6 @@ static inline v3 ray_at(const ray_t *r, float t) { return vadd(r->A, vscale(t, r
 #define LCG_A 0x5DEECE66Dull
 #define LCG_C 0xBull
 #define LCG_M 0xFFFFFFFFFFFFull
-static const uint64_t kGamma = 0x9E3779B97F4A7C15ull;
 
 static inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -66,13 +65,13 @@ static inline uint64_t mix64(uint64_t z) {
 static inline uint64_t sample_key(uint64_t seed, uint32_t pixel, uint32_t sample) {
     return mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) ^ (((uint64_t)pixel << 32) | sample));
 }
-static inline double u48(uint64_t z) { return (double)(z >> 16) * 0x1p-48; }
 
 typedef struct {
     int counter;
     uint64_t x;      /* canonical LCG state */
     uint64_t key;    /* counter: sample key (the medium stream's seed) */
     uint64_t n;      /* unused */
+    int nmedia;      /* counter: the scene's constant_media (the medium stream's stride per segment) */
 } rng_t;
 
 /* drand48's step (x = a x + c mod 2^48, draw = x / 2^48) in both modes: canonical is
@@ -87,11 +86,25 @@ static inline void rng_seed_sample(rng_t *g, uint64_t key) {
     g->x = key & LCG_M;
     g->n = 0;
 }
+/* x advanced n drand48 steps at once: x_n = A^n x + C (A^(n-1) + ... + 1) mod 2^48,
+ * by squaring (the kernel walks the same sequence one step per medium and segment). */
+static inline uint64_t lcg_skip(uint64_t x, uint64_t n) {
+    uint64_t a = LCG_A, c = LCG_C, A = 1, C = 0;
+    for (; n; n >>= 1) {
+        if (n & 1) { A = (A * a) & LCG_M; C = (C * a + c) & LCG_M; }
+        c = (c * (a + 1)) & LCG_M;
+        a = (a * a) & LCG_M;
+    }
+    return (A * x + C) & LCG_M;
+}
+/* The constant_medium draw of medium k (list order) at segment `bounce` of the sample:
+ * the medium stream is drand48's generator started at mix64(key ^ 0xD1B5..) mod 2^48
+ * and stepped once per medium per segment, whether or not the medium draws, so draw
+ * (bounce, k) is the stream's (bounce * nmedia + k + 1)-th value. */
 static inline double rng_medium(rng_t *g, int bounce, int k) {
     if (!g->counter) return rng_next(g);
-    uint64_t mk = mix64(g->key ^ 0xD1B54A32D192ED03ull);
-    uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
-    return u48(mix64(mk + (m + 1) * kGamma));
+    uint64_t x0 = mix64(g->key ^ 0xD1B54A32D192ED03ull) & LCG_M;
+    return (double)lcg_skip(x0, (uint64_t)bounce * (uint64_t)g->nmedia + (uint64_t)k + 1) * 0x1p-48;
 }
 
 /* ---------------------------------------------------------------- Perlin */
@@ -846,7 +859,10 @@ static v3 render_pixel(run_t *rn, const cam_t *cam, int i, int j, rng_t *g) {
     int chunk = p->chunk > 0 ? p->chunk : p->ns;
     v3 col = V(0, 0, 0), part = V(0, 0, 0);
     for (int s = 0; s < p->ns; s++) {
-        if (g->counter) rng_seed_sample(g, sample_key(p->seed, (uint32_t)(j * p->nx + i), (uint32_t)s + p->sample_offset));
+        if (g->counter) {
+            rng_seed_sample(g, sample_key(p->seed, (uint32_t)(j * p->nx + i), (uint32_t)s + p->sample_offset));
+            g->nmedia = rn->sc->nmedia;
+        }
         float u = (float)(i + rng_next(g)) / (float)p->nx;                /* main.cpp:305-306 */
         float v = (float)(j + rng_next(g)) / (float)p->ny;
         ray_t r = camera_get_ray(cam, u, v, g);
@@ -953,8 +969,9 @@ void oracle_counter_draws(uint64_t seed, uint32_t pixel, uint32_t sample, int n,
     for (int i = 0; i < n; i++) out[i] = rng_next(&g);
 }
 
-double oracle_medium_draw(uint64_t seed, uint32_t pixel, uint32_t sample, int bounce, int medium) {
+double oracle_medium_draw(uint64_t seed, uint32_t pixel, uint32_t sample, int bounce, int medium, int nmedia) {
     rng_t g; memset(&g, 0, sizeof g); g.counter = 1; rng_seed_sample(&g, sample_key(seed, pixel, sample));
+    g.nmedia = nmedia;
     return rng_medium(&g, bounce, medium);
 }
 

@@ -71,8 +71,10 @@ __device__ __forceinline__ V3 at(const Ray &r, float t) { return add(r.o, scale(
 // Per-sample drand48 streams: sample (pixel, s) runs drand48's own
 // generator (x = a x + c mod 2^48, draw = x / 2^48; the reference's drand48,
 // main.cpp:305-306, camera.h:45-53, material.h:44-118) from x0 = key mod 2^48, key =
-// mix64(seed_key ^ (pixel << 32 | s)); constant_medium draws come from a second keyed
-// stream.  Random access for the cooperative samplers: x_{n+j} = A_j x_n + C_j, with
+// mix64(seed_key ^ (pixel << 32 | s)); constant_medium draws come from a second
+// drand48 stream of the sample, from mix64(key ^ 0xD1B5..) mod 2^48, stepped once per
+// medium and segment whether or not the medium draws (media_hit), so the draw of
+// medium k at segment d is its (d * nmedia + k + 1)-th value.  Random access for the cooperative samplers: x_{n+j} = A_j x_n + C_j, with
 // (A_j, C_j) from a table (RT_LCG_JUMPS entries, LDS).
 constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t kLcgA = 0x5DEECE66Dull, kLcgC = 0xBull, kLcgM = 0xFFFFFFFFFFFFull;
@@ -135,20 +137,16 @@ __device__ __forceinline__ uint64_t sample_key(uint64_t skey, uint32_t pixel, ui
 }
 struct Rng {
     uint64_t x;      // the sample's drand48 state
-    uint64_t mkey;   // medium stream key, derived once per sample
-    // media = false: the scene has no constant_medium, so the medium key is never read
+    uint64_t xm;     // its medium stream's state (media_hit steps it once per medium and segment)
+    // media = false: the scene has no constant_medium, so the medium stream is never read
     __device__ __forceinline__ void start(uint64_t k, bool media = true) {
         x = k & kLcgM;
-        mkey = media ? mix64(k ^ 0xD1B54A32D192ED03ull) : 0;
+        xm = media ? mix64(k ^ 0xD1B54A32D192ED03ull) & kLcgM : 0;
     }
     __device__ __forceinline__ double next() { x = lcg_step(x); return u48x(x); }
     __device__ __forceinline__ void skip() { x = lcg_step(x); }   // a draw whose value is not used
     __device__ __forceinline__ void skip2() { x = lcg_step(lcg_step(x)); }   // two of them (a constant jump's
                                                                             // 64-bit addend got hoisted and spilled)
-    __device__ __forceinline__ double medium(int bounce, int k) const {
-        uint64_t m = ((uint64_t)bounce << 8) | (uint64_t)k;
-        return u48(mix64(mkey + (m + 1) * kGamma));
-    }
 };
 
 // Natural log in double for x in [0, 1) — constant_medium's log(drand48())
@@ -1390,7 +1388,7 @@ __device__ __forceinline__ void load_media(const RtKernelArgs &A, MediumRec *lds
 // One medium's test (constant_medium.h:26-50) against the surface result.
 template <bool kCount, bool kInst = true>
 __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRec &M, int k, const Ray &r, const Recip &rd,
-                                           const Recip &ra, int depth, const Rng &g, bool &have, float &best_t,
+                                           const Recip &ra, uint64_t xk, bool &have, float &best_t,
                                            int &med_mat, LdsMediaConsts *mc, Counters &cnt) {
     const float dlen = rd.a;
     if (kCount) cnt.media++;
@@ -1434,7 +1432,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     r1 = r1 < 0 ? 0.f : r1;
     const float distance_inside_boundary = (r2 - r1) * dlen;
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
-    const float hit_distance = (float)((double)neg_inv_density * log_f64(g.medium(depth, k), mc->c02));
+    const float hit_distance = (float)((double)neg_inv_density * log_f64(u48x(xk), mc->c02));
     const bool hit = ok && hit_distance < distance_inside_boundary;
     const float tm = r1 + div_by(hit_distance, rd);
     best_t = hit ? tm : best_t;
@@ -1448,7 +1446,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
 // issue generic (flat) loads, which wait on both memory counters.
 template <bool kCount, bool kInst = true>
 __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec *lds_media, LdsMediaConsts *mc, const Ray &r,
-                                         const Recip &rd, int depth, const Rng &g, bool &have, float &best_t, Counters &cnt) {
+                                         const Recip &rd, Rng &g, bool &have, float &best_t, Counters &cnt) {
     // a = |d|^2 of the boundary spheres' quadratics (sphere.h:28), its reciprocal once for all media
     const Recip ra = recip_of(dot(r.d, r.d), true);
     typedef unsigned U4v __attribute__((ext_vector_type(4)));
@@ -1462,14 +1460,16 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
         M.md = make_int4((int)x.x, (int)x.y, (int)x.z, (int)x.w);
         M.g0 = make_float4(__uint_as_float(y.x), __uint_as_float(y.y), __uint_as_float(y.z), __uint_as_float(y.w));
         M.mm = make_float4(__uint_as_float(z.x), __uint_as_float(z.y), __uint_as_float(z.z), __uint_as_float(z.w));
-        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, mc, cnt);
+        g.xm = lcg_step(g.xm);   // this medium's draw, taken or not
+        medium_one<kCount, kInst>(A, M, k, r, rd, ra, g.xm, have, best_t, med_mat, mc, cnt);
     }
     for (int k = RT_LDS_MEDIA; k < A.nmedia; ++k) {
         MediumRec M;
         M.md = A.media[k];
         M.g0 = A.bprims[M.md.x * 4 + 0];
         M.mm = A.bprims[M.md.x * 4 + 1];
-        medium_one<kCount, kInst>(A, M, k, r, rd, ra, depth, g, have, best_t, med_mat, mc, cnt);
+        g.xm = lcg_step(g.xm);
+        medium_one<kCount, kInst>(A, M, k, r, rd, ra, g.xm, have, best_t, med_mat, mc, cnt);
     }
     return med_mat;
 }

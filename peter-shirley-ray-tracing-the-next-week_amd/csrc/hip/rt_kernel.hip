@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     r.o = mk(0, 0, 0); r.d = mk(0, 0, 0); r.time = 0;
     V3 beta = mk(1, 1, 1);
     int depth = 0;
-    Rng g; g.x = 0; g.mkey = 0;
+    Rng g; g.x = 0; g.xm = 0;
     // this lane's pre-made sample start, taken by retire_and_claim for camera_begin
     // (read out at once: a refill later in the same claim reuses the slots)
     bool pre_have = false;
@@ -520,8 +520,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
-            const int med_mat = kMedia ? media_hit<kCount, kInst>(A, lds_media, (LdsMediaConsts *)&lds_mconst, r, rd, depth, g,
-                                                                  have, best_t, cnt)
+            const int med_mat = kMedia ? media_hit<kCount, kInst>(A, lds_media, (LdsMediaConsts *)&lds_mconst, r, rd, g, have,
+                                                                  best_t, cnt)
                                        : -1;
             if (med_mat >= 0) {
                 hr.p = at(r, best_t);

@@ -49,7 +49,7 @@ int main(void) {
     double d[64];
     oracle_drand48(0, 64, d);
     oracle_counter_draws(1, 2, 3, 64, d);
-    (void)oracle_medium_draw(1, 2, 3, 4, 5);
+    (void)oracle_medium_draw(1, 2, 3, 4, 5, 6);
     float ranvec[768];
     int32_t perm[768];
     oracle_perlin_tables(ranvec, perm);
