@@ -838,13 +838,21 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
 #ifndef RT_DESCEND_TAIL2
 #define RT_DESCEND_TAIL2 8
 #endif
+#ifndef RT_DESCEND_TAIL_DRY
+#define RT_DESCEND_TAIL_DRY 0
+#endif
 // kPark2 (the cooperative leaf tests, coop_leaves): a lane holding a parked leaf
 // parks a second one too when both together hold at most RT_MAX_LEAF primitives
 // (pleaf2), so a round's pair list is longer and rounds are fewer.
+// dry = true (a wave draining the launch's last paths, few lanes live): no tail cut —
+// the cut trades a few lanes' node steps for the others', and with a handful of lanes
+// every round's fixed cost (slab set-up, leaf pass, exit checks) is on the path's
+// latency, which is what the launch's end waits for.
 template <int kWidth, bool kCount, int kSteps = 1, bool kPark2 = false, class Nodes>
 __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, const Slab &sl, float best_t,
-                                            uint32_t *stk, int &sp, Counters &cnt, uint32_t *pleaf2 = nullptr) {
-    constexpr int kTail = kSteps == 1 ? RT_DESCEND_TAIL : RT_DESCEND_TAIL2;
+                                            uint32_t *stk, int &sp, Counters &cnt, uint32_t *pleaf2 = nullptr,
+                                            bool dry = false) {
+    const int kTail = dry ? RT_DESCEND_TAIL_DRY : (kSteps == 1 ? RT_DESCEND_TAIL : RT_DESCEND_TAIL2);
     uint32_t pleaf = RT_EMPTY_CHILD, pl2 = RT_EMPTY_CHILD;
     for (;;) {
 #pragma unroll

@@ -67,6 +67,12 @@ namespace {
 #define RT_COOP_PARK2 0
 #endif
 
+// A wave whose claims found the pool dry and that holds at most this many live paths
+// runs latency-first (descend's tail cut off)
+#ifndef RT_DRY_LANES
+#define RT_DRY_LANES 16
+#endif
+
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
@@ -379,7 +385,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // cooperative rounds: a metal's absorbed reflection; the others start their
         // next sample inside stage 5)
         retire_and_claim();
-        if (wballot(!finished) == 0ull) break;
+        const uint64_t live = wballot(!finished);
+        if (live == 0ull) break;
+        // the pool is dry and few paths are left: the launch's end waits on their latency
+        const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
         {
             const bool starting = phase == PH_IDLE && !finished;
             float cu_ = 0, cv_ = 0;
@@ -461,9 +470,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     uint32_t pleaf;
                     if constexpr (kLds && RT_LDS_SIGNED && kWidth == 2) lnodes.prepare(sl);
                     if constexpr (kLds)
-                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt);
+                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt,
+                                                                                      nullptr, dry);
                     else
-                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt);
+                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt,
+                                                                                      nullptr, dry);
                     if (kCount && RT_COOP_STATS) {   // experiment: leaf rounds and their primitives
                         const uint64_t own = wballot(pleaf != RT_EMPTY_CHILD);
                         const uint32_t n = pleaf != RT_EMPTY_CHILD ? RT_LEAF_COUNT(pleaf) : 0u;
