@@ -600,8 +600,10 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
 
 // Partial-sum slab budget per launch (bytes; env RTNW_SLAB_BUDGET overrides, for tests).
 // A job whose slab would be larger runs as several launches over sample batches.
+// 16 GiB of the 288 GiB HBM: config 5 on one GPU (1e9 samples, 12 GB) is one launch,
+// one launch-end drain; 8 GiB made it two.
 #ifndef RT_SLAB_BUDGET
-#define RT_SLAB_BUDGET (8ull << 30)
+#define RT_SLAB_BUDGET (16ull << 30)
 #endif
 static uint64_t slab_budget() {
     if (const char *e = std::getenv("RTNW_SLAB_BUDGET")) {
