@@ -12,16 +12,23 @@
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-CFG=${1:-c4}   # the bench config profiled (c4 = the metric's; c2, c3, c5 for their own bench lines)
+CFG=${1:-c4}   # the bench config profiled (c4 = the metric's; c2, c3, c5 for their own bench lines;
+               # c5_nN: one rank's share of c5 split over N GPUs, bench.py --share-of N)
 O=gpurun_out/final_$CFG
 mkdir -p $O/classes
-B="python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline"
+case $CFG in
+  c5_n*) B="python3 bench.py --share-of ${CFG#c5_n} --steps 1 --warmup 0 --no-cpu-baseline" ;;
+  *)     B="python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline" ;;
+esac
 for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:l2" \
             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE:sq"; do
   ctrs=${pass%%:*}; name=${pass##*:}
   echo "== pmc $name"
   timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/pmc_$name -o run --output-format csv -- $B > $O/pmc_$name.log 2>&1
 done
+echo "== pmc lanes"   # VALU lane utilisation (tools/lanes_summary.py reads gpurun_out/lanes_<cfg>)
+timeout -s KILL 240 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/lanes_$CFG -o run \
+    --output-format csv -- $B > $O/pmc_lanes.log 2>&1
 i=0
 for ctrs in "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT" \
             "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_BRANCH"; do

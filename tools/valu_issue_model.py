@@ -160,7 +160,7 @@ def main():
     samples = float(sys.argv[5]) if len(sys.argv) > 5 else 250e6
     config = sys.argv[6] if len(sys.argv) > 6 else "c4"
     clock_hz = float(sys.argv[7]) * 1e9 if len(sys.argv) > 7 and sys.argv[7] else CLOCK_HZ
-    symbol = SYMBOLS[config]
+    symbol = SYMBOLS[config.split("_n")[0]]   # c5_nN: a rank's share of c5, the same kernel
     costs = measured_costs(rates)
     ops = static_opcodes(isa, symbol)
     per_class = collections.defaultdict(lambda: [0, 0.0])   # static count, static count x cost
