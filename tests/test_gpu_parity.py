@@ -24,11 +24,12 @@ pytestmark = pytest.mark.gpu
 TOL_RMS = 1e-3
 # Bit-exact fraction of the framebuffer floats against the oracle.  What differs
 # is ocml vs glibc sinf / log / pow last bits, which now and then send one sample
-# down another path; a pixel is bit-exact only if ALL its samples are, so the bar is
-# per sample: at most 1 in 2,000 samples may differ (measured: 1 in 2,800 at 8 spp,
-# smoke 0.9971; 1 in 6,300 at 1000 spp, the c4 centre crop 0.854 = 55 of 64 pixels).
-# Capped at 0.99 of the pixels, so a low-spp case that breaks more than 1 % of the
-# pixels' bits fails.
+# down another path; a pixel is bit-exact only if ALL its samples are.  The bar:
+# >= 99 % of the pixels up to 20 spp (measured minimum 0.9902, the `test` scene at 8
+# spp; smoke 0.9964), and above that 0.9995^spp, i.e. at most ~1 sample in 2,000
+# differing (measured: the c4 / c5 centre crops at 1000 spp, 0.82-0.88 of 64 pixels,
+# ~1 sample in 5,000-7,000).  A change that breaks more than 1 % of a low-spp image's
+# pixels fails here.
 EXACT_PER_SAMPLE = 0.9995
 
 
