@@ -3,7 +3,7 @@
  * fma(r, y, q) must equal the IEEE quotient RN(x/b) (Markstein's theorem) for every
  * x, b whose reciprocal and quotient are normal floats.  Random pairs over a wide
  * exponent range plus the kernel's own shapes: image coordinates (px + u) / nx,
- * normals (p - c) / r, unit vectors d / |d|, ray distances / |d|^2.
+ * normals (p - c) / r, unit vectors d / |d|, ray distances / |d|^2, sphere roots.
  * Usage: div_rn_check [N]; prints the mismatch count, exit status 1 on any. */
 #include <math.h>
 #include <stdint.h>
@@ -48,7 +48,16 @@ int main(int argc, char **argv) {
         float len = sqrtf(a * a + c * c + d * d);
         check(a, len);                                                          /* unit vector */
         check(rf(-10, 14), a * a + c * c + d * d);                              /* distance / |d|^2 */
+        {   /* a sphere's roots (-b -+ sqrt(disc)) / |d|^2, sphere.h:33-40 (prim_t_head, sphere_t) */
+            float ox = rf(-2, 10), oy = rf(-2, 10), oz = rf(-2, 10), rad = rf(-4, 10);
+            float aa = a * a + c * c + d * d, bb = ox * a + oy * c + oz * d;
+            float cc = ox * ox + oy * oy + oz * oz - rad * rad, disc = bb * bb - aa * cc;
+            if (disc > 0) {
+                check(-bb - sqrtf(disc), aa);
+                check(-bb + sqrtf(disc), aa);
+            }
+        }
     }
-    printf("%ld mismatches in %ld x 5 divisions\n", bad, n);
+    printf("%ld mismatches in %ld x 5-7 divisions\n", bad, n);
     return bad != 0;
 }
