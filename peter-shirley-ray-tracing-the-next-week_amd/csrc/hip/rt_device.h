@@ -1127,12 +1127,24 @@ __device__ __forceinline__ CamView load_camera(const CamV4 *lds) {
 // hitable_list's acceptance (hitable_list.h:20-32: `t < closest`, ties to the earlier
 // list entry, the key) as selects: bitwise operators, so no short-circuit branches and
 // no exec-mask juggling around three moves per tested primitive.
+// kPacked (the LDS-BVH variants, < 2^15 primitives, RT_PACKED_BEST): best_prim holds
+// (key + 2^15) << 16 | primitive — the key's order in the high half, so one unsigned
+// compare decides a tie — and best_key is not used: one register and one select
+// fewer per test.  "Nothing found" is 0xFFFFFFFF, above every packed candidate.
+template <bool kPacked = false>
 __device__ __forceinline__ void keep_closest(bool in, float t, int key, uint32_t idx, float &best_t, int &best_key,
                                              uint32_t &best_prim) {
-    const bool take = in & ((t < best_t) | ((t == best_t) & (key < best_key)));
-    best_t = take ? t : best_t;
-    best_key = take ? key : best_key;
-    best_prim = take ? idx : best_prim;
+    if constexpr (kPacked) {
+        const uint32_t kp = ((uint32_t)(key + 0x8000) << 16) | idx;
+        const bool take = in & ((t < best_t) | ((t == best_t) & (kp < best_prim)));
+        best_t = take ? t : best_t;
+        best_prim = take ? kp : best_prim;
+    } else {
+        const bool take = in & ((t < best_t) | ((t == best_t) & (key < best_key)));
+        best_t = take ? t : best_t;
+        best_key = take ? key : best_key;
+        best_prim = take ? idx : best_prim;
+    }
 }
 
 // ------------------------------------------------------ cooperative leaf tests
@@ -1141,7 +1153,7 @@ __device__ __forceinline__ void keep_closest(bool in, float t, int key, uint32_t
 // any t_min works; a miss, RT_INF, is never packed), then the list-order key
 // biased into 16 bits, then the primitive (keys are unique, so it never decides).
 // The LDS-BVH variant only: the host keeps those scenes below 2^15 primitives
-// (capi.cpp, RT_COOP_MAX_PRIMS).  "Nothing found" (best_prim = ~0) packs as an
+// (capi.cpp, RT_LDS_MAX_PRIMS).  "Nothing found" (best_prim = ~0) packs as an
 // all-ones low word, above every real key at the same t.
 __device__ __forceinline__ uint32_t ford(float t) {
     const uint32_t b = __float_as_uint(t);
@@ -1263,7 +1275,7 @@ __device__ __forceinline__ void coop_leaves(uint32_t pleaf, uint32_t pleaf2, con
 // instance chain; otherwise the caller transformed `r`.  Used by the BVH modes'
 // pre-scan; the flat scan, whose groups are ordered by kind, runs scan_group below.
 typedef __attribute__((address_space(4))) const F4v ConstF4;   // uniform index: scalar (SMEM) loads
-template <bool kCount, bool kInst, bool kPerPrimInst, class PT>
+template <bool kCount, bool kInst, bool kPerPrimInst, bool kPacked = false, class PT>
 __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const float4 *insts,
                                                const Ray &r, float tmin, bool in, int group_inst, float &best_t,
                                                int &best_key, uint32_t &best_prim, Counters &cnt) {
@@ -1286,7 +1298,7 @@ __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const
         const int key = kind <= RT_PRIM_MOVING_SPHERE ? order : -1 - order;
         if (kCount && in) cnt.prim(kind | (kInst && inst >= 0 ? 0x100 : 0));
         if (kCount && first_active()) cnt.w_prims++;
-        keep_closest(in, t, key, (uint32_t)q, best_t, best_key, best_prim);
+        keep_closest<kPacked>(in, t, key, (uint32_t)q, best_t, best_key, best_prim);
     }
 }
 

@@ -14,7 +14,7 @@
 #define RT_LDS_NODE_BYTES (4 * RT_LDS_NODE_CAP * 16)
 #define RT_LDS_STACK_BYTES(depth) ((RT_LDS_BLOCK / 64) * (depth) * 64 * 4)
 #define RT_LDS_BUDGET 163840   // LDS bytes per CU (160 KiB)
-#define RT_COOP_MAX_PRIMS 32767  // LDS variant: surface primitives (keys and indices packed in 16 bits)
+#define RT_LDS_MAX_PRIMS 32767   // LDS variant: surface primitives (closest-hit key and index packed in 16 bits each)
 
 // scene features a megakernel variant carries code for (rt_launch_megakernel)
 #define RT_FEAT_INST 1      // translate / rotate_y / flip_normals chains

@@ -73,6 +73,18 @@ namespace {
 #define RT_DRY_LANES 16
 #endif
 
+// An item's radiance sum kept in its slab record instead of three registers held
+// across the persistent loop (end_path); 0: summed in registers, stored at retire
+#ifndef RT_SLAB_DIRECT
+#define RT_SLAB_DIRECT 0
+#endif
+
+// LDS-BVH variants: the closest hit's list-order key and primitive packed in one
+// register (rt_device.h keep_closest<kPacked>; capi.cpp keeps those scenes < 2^15 primitives)
+#ifndef RT_PACKED_BEST
+#define RT_PACKED_BEST 0
+#endif
+
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
@@ -124,6 +136,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
     // the LDS-BVH2 variant tests its parked leaves with the whole wave (coop_leaves)
     constexpr bool kCoopLeaf = RT_COOP_LEAF && kLds && kWidth == 2 && RT_LDS_SIGNED;
+    // the closest hit's key and primitive in one register (keep_closest<kPacked>)
+    constexpr bool kPacked = RT_PACKED_BEST && kLds && !kCoopLeaf;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
     __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : (kWidth >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH)][64];
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
@@ -290,10 +304,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // the next pre-made sample starts (one global atomic per A.claim items)
     auto retire_and_claim = [&]() {
         if (phase == PH_IDLE && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
+#if !RT_SLAB_DIRECT
             float *sl = A.slab + (size_t)item * RT_SLAB_FLOATS;   // 12 B per item (16 with RT_SLAB_F4)
             sl[0] = part.x;
             sl[1] = part.y;
             sl[2] = part.z;
+#endif
             item = 0xFFFFFFFFu;
         }
         bool need = phase == PH_IDLE && !finished && item == 0xFFFFFFFFu;
@@ -371,7 +387,18 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (!(L.x == L.x)) L.x = 0;
         if (!(L.y == L.y)) L.y = 0;
         if (!(L.z == L.z)) L.z = 0;
+#if RT_SLAB_DIRECT
+        // the item's sum lives in its slab record, not in registers across the loop: the
+        // first sample stores (0 + L == L bitwise: L >= +0 after de_nan), later samples of
+        // a multi-sample item add to what this lane stored (main.cpp:311's order)
+        float *sl = A.slab + (size_t)item * RT_SLAB_FLOATS;
+        if (A.chunk > 1 && (uint32_t)s_cur % (uint32_t)A.chunk != 0u) L = add(mk(sl[0], sl[1], sl[2]), L);
+        sl[0] = L.x;
+        sl[1] = L.y;
+        sl[2] = L.z;
+#else
         part = add(part, L);
+#endif
         ++s_cur;
         phase = PH_IDLE;
     };
@@ -444,7 +471,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             if (kPrescan && A.nprescan > 0) {
                 const bool fr = fresh && phase == PH_TRAV;
                 if (wballot(fr) != 0ull)
-                    lockstep_prims<kCount, kInst, true>((const ConstF4 *)A.prims, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
+                    lockstep_prims<kCount, kInst, true, kPacked>((const ConstF4 *)A.prims, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
                                                         best_t, best_key, best_prim, cnt);
                 fresh = false;
             }
@@ -496,11 +523,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                                 int key, kind;
                                 float t = prim_t_head<kInst, kK>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
                                 if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                                keep_closest(true, t, key, ia, best_t, best_key, best_prim);
+                                keep_closest<kPacked>(true, t, key, ia, best_t, best_key, best_prim);
                                 if (two) {
                                     t = prim_t_head<kInst, kK>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
                                     if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                                    keep_closest(true, t, key, ib, best_t, best_key, best_prim);
+                                    keep_closest<kPacked>(true, t, key, ib, best_t, best_key, best_prim);
                                 }
                             };
                             // the kinds the wave tests in this pass: a wave of spheres only or of
@@ -539,7 +566,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 hr.n = mk(1, 0, 0);
                 hr.mat = med_mat;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
             } else if (have) {
-                hr = prim_record<kInst, kUV>(A.prims, A.insts, A.mats, best_prim, r, best_t);
+                hr = prim_record<kInst, kUV>(A.prims, A.insts, A.mats, kPacked ? best_prim & 0xFFFFu : best_prim, r, best_t);
             }
         }
 

@@ -570,10 +570,10 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             lds_cu = 0;
         const long stat = std::max<long>(rt_megakernel_lds_static_bytes(), rt_megakernel_lds_static_actual());
         const long need_actual = need - rt_megakernel_lds_static_bytes() + stat;
-        // (its cooperative leaf tests pack the list-order key and the primitive index
-        // into 16 bits each, rt_device.h pack_hit: fewer than RT_COOP_MAX_PRIMS primitives)
+        // (it carries the closest hit's list-order key and primitive index in 16 bits
+        // each, rt_device.h keep_closest<kPacked> / pack_hit: fewer than RT_LDS_MAX_PRIMS)
         s->lds_nodes = want && !s->scan && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
-                       s->nnodes <= RT_LDS_NODE_CAP && d->nprims < RT_COOP_MAX_PRIMS &&
+                       s->nnodes <= RT_LDS_NODE_CAP && d->nprims < RT_LDS_MAX_PRIMS &&
                        need_actual <= std::min<long>(RT_LDS_BUDGET, lds_cu);
         if (s->lds_nodes)
             for (int mode = 0; mode < 3; mode++) s->grid[mode] = s->cus;
