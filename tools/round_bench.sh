@@ -1,3 +1,5 @@
+# tools/round_bench.sh — the round's bench evidence on the gpurun box: tools/final_bench.sh (kernel
+# trace + bench lines), the c4 wave timeline and the final() stage profile.
 set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
