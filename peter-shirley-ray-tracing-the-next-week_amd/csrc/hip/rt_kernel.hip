@@ -231,6 +231,13 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     uint64_t rt_exhaust = 0;
     uint32_t rt_items = 0;   // work items this wave claimed (kProf)
     auto mark = [&](int k) {
+#ifdef RT_ASM_MARKS
+        if (k == 0) asm volatile("; @@MARK 0" ::: "memory");
+        else if (k == 1) asm volatile("; @@MARK 1" ::: "memory");
+        else if (k == 2) asm volatile("; @@MARK 2" ::: "memory");
+        else if (k == 3) asm volatile("; @@MARK 3" ::: "memory");
+        else asm volatile("; @@MARK 4" ::: "memory");
+#endif
         if (kProf) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             prof[k] += now - stamp;
