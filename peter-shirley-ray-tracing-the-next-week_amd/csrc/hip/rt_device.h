@@ -96,19 +96,44 @@ __device__ __forceinline__ double u48x(uint64_t x) {
 }
 // One drand48 step, mod 2^48 with 32-bit operations: a = 5 * 2^32 + 0xDEECE66D, x =
 // xh * 2^32 + xl (xh < 2^16), so a x = 0xDEECE66D xl + (5 xl + 0xDEECE66D xh) 2^32
-// (mod 2^48): one v_mad_u64_u32 (+ c), two 32-bit multiply-adds into the high word.
+// (mod 2^48): one v_mad_u64_u32 (+ c) and two multiply-adds into the high word, of
+// which only 16 bits are kept — so 16 x 16-bit products suffice (v_mad_u32_u16).
+// RT_LCG_ASM (default 1) spells the four instructions out: from the C form the compiler
+// built the high word as a 64-bit sum (three v_mad_u64_u32, two of them by 0, a 64-bit
+// add and two moves).  The same values either way (the GPU parity tests are bitwise).
+#ifndef RT_LCG_ASM
+#define RT_LCG_ASM 1
+#endif
 __device__ __forceinline__ uint64_t lcg_step(uint64_t x) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+#if RT_LCG_ASM
+    static_assert(kLcgC == 11, "the drand48 increment is the inline constant of v_mad_u64_u32 below");
+    uint64_t p, cy;   // cy: the carry-out SGPR pair gfx9 requires (unused)
+    uint32_t hi;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 11" : "=v"(p), "=s"(cy) : "v"(xl), "s"(0xDEECE66Du));
+    asm("v_mad_u32_u16 %0, %1, 5, %2" : "=v"(hi) : "v"(xl), "v"((uint32_t)(p >> 32)));
+    asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(hi) : "v"(xh), "s"(0xE66Du), "v"(hi));
+#else
     const uint64_t p = (uint64_t)xl * 0xDEECE66Du + kLcgC;
     const uint32_t hi = (uint32_t)(p >> 32) + xl * 5u + xh * 0xDEECE66Du;
+#endif
     return ((uint64_t)(hi & 0xFFFFu) << 32) | (uint32_t)p;
 }
 // j steps at once: x_{n+j} = A_j x_n + C_j (mod 2^48); jt = (A_j lo, A_j hi, C_j lo, C_j hi)
 typedef unsigned U4j __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint64_t lcg_jump(uint64_t x, U4j jt) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-    const uint64_t p = (uint64_t)xl * jt.x + (((uint64_t)jt.w << 32) | jt.z);   // wraps mod 2^64: only 48 bits kept
+    const uint64_t c = ((uint64_t)jt.w << 32) | jt.z;
+#if RT_LCG_ASM
+    uint64_t p, cy;
+    uint32_t hi;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(p), "=s"(cy) : "v"(xl), "v"(jt.x), "v"(c));   // wraps mod 2^64: 48 bits kept
+    asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(hi) : "v"(xl), "v"(jt.y), "v"((uint32_t)(p >> 32)));
+    asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(hi) : "v"(xh), "v"(jt.x), "v"(hi));
+#else
+    const uint64_t p = (uint64_t)xl * jt.x + c;   // wraps mod 2^64: only 48 bits kept
     const uint32_t hi = (uint32_t)(p >> 32) + xl * jt.y + xh * jt.x;
+#endif
     return ((uint64_t)(hi & 0xFFFFu) << 32) | (uint32_t)p;
 }
 // Jumps of 0 .. RT_LCG_JUMPS - 1 steps: a cooperative round's candidate t of an owner

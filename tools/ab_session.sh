@@ -1,9 +1,16 @@
-# tools/ab_session.sh — one A/B session on the gpurun box (edit the variants): tools/ab.py over
-# libraries / environment settings (c4; @--config+c3 for c3, @--share-of+8 for a c5 rank share).
+#!/bin/bash
+# tools/ab_session.sh — one A/B session on the gpurun box (edit the variants): the GPU
+# parity tests with the in-tree library, then tools/ab.py over libraries / environment
+# settings (c4; @--config+c3 for c3, @--share-of+8 for a c5 rank share).
 set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
-L=variants/cur/librt_hip.so
-timeout -k 10 1100 python3 tools/ab.py $L $L:RTNW_TAIL_CLAIMS=16 $L:RTNW_TAIL_CLAIMS=64 $L:RTNW_TAIL_CLAIMS=128 $L:RTNW_CLAIM=4 $L:RTNW_CLAIM=16 "$L@--share-of+8" "$L:RTNW_TAIL_CLAIMS=64@--share-of+8" "$L:RTNW_TAIL_CLAIMS=128@--share-of+8" --rounds 3 > gpurun_out/ab15.log 2>&1
-echo "ab rc=$?"; grep SUMMARY gpurun_out/ab15.log
+TAG=${1:-ab}
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 120 --timeout-method thread \
+    > gpurun_out/${TAG}_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
+tail -1 gpurun_out/${TAG}_tests.log
+C=variants/lcga/librt_hip.so; A=variants/nosq/librt_hip.so; B=variants/all3/librt_hip.so
+timeout -k 10 900 python3 tools/ab.py $C $A $B "$C@--config+c3" "$A@--config+c3" "$B@--config+c3" \
+    "$C@--share-of+8" "$B@--share-of+8" "$C@--config+c2" "$B@--config+c2" --rounds 3 > gpurun_out/${TAG}.log 2>&1
+echo "ab rc=$?"; grep SUMMARY gpurun_out/${TAG}.log

@@ -10,7 +10,7 @@ build_one() {
   local name=$1 defs=$2
   mkdir -p ../variants/$name
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -I../include -Icsrc -Icsrc/host --offload-arch=gfx950 \
-      -Icsrc/hip -munsafe-fp-atomics $defs -c "${RT_SRC:-csrc/hip/rt_kernel.hip}" -o ../variants/$name/rt_kernel.o \
+      -Icsrc/hip -munsafe-fp-atomics -cuid=rt_kernel $defs -c "${RT_SRC:-csrc/hip/rt_kernel.hip}" -o ../variants/$name/rt_kernel.o \
       -Rpass-analysis=kernel-resource-usage 2> ../variants/$name/resource.txt
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o ../variants/$name/librt_hip.so ../variants/$name/rt_kernel.o \
       build/capi.o build/bvh.o build/flatten.o build/rtnw.o build/png.o build/dist.o -lz -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
