@@ -1520,6 +1520,9 @@ __device__ __forceinline__ int media_hit(const RtKernelArgs &A, const MediumRec 
 }
 
 // ------------------------------------------------------------------ shade
+#ifndef RT_SHADE_LEAN
+#define RT_SHADE_LEAN 5   // bits: 1 scatter outputs, 2 hit record (spills: off), 4 texture value
+#endif
 struct ShadeOut {
     bool scattered;
     V3 att, emitted;
@@ -1544,7 +1547,9 @@ __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool re
     ShadeState st;
     st.kind = -1;
     st.live = false;
-    st.tv = mk(0, 0, 0);
+#if !(RT_SHADE_LEAN & 4)
+    st.tv = mk(0, 0, 0);   // (lean: set for the textured and noisy lanes, the only readers)
+#endif
     bool noisy = false;
     float nscale = 0.f;
     if (shading) {
@@ -1598,9 +1603,14 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
                                                  const Hit &hr, const ShadeState &st, V3 rius, Rng &g) {
     ShadeOut o;
     o.scattered = false;
-    o.att = mk(0, 0, 0);
     o.emitted = mk(0, 0, 0);
+#if !(RT_SHADE_LEAN & 1)
+    o.att = mk(0, 0, 0);
     o.ray = r;
+#endif
+    // RT_SHADE_LEAN: o.att and o.ray are set by the scattering branches only (the caller
+    // reads them only when o.scattered): default copies of the ray, kept alive down every
+    // early return, were ~30 register moves per wave iteration
     const int kind = st.kind;
     // unit(r.d) (vec3.h:146) once, for the lanes whose scatter needs it (metal,
     // dielectric) instead of once in each of their branches
@@ -1612,7 +1622,11 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
     if (!have || !st.live) return o;
     const float4 m0 = A.mats[hr.mat * 2 + 0];
     const float4 m1 = A.mats[hr.mat * 2 + 1];
+#if RT_SHADE_LEAN & 1
+    Ray ns;
+#else
     Ray ns = r;
+#endif
     if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
         V3 target = add(add(hr.p, hr.n), rius);
         ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;

@@ -125,6 +125,9 @@ __device__ __forceinline__ KArgs *opaque_kargs(KArgs *p) {
     return p;
 }
 
+#ifndef RT_MERGE_SEG
+#define RT_MERGE_SEG 1
+#endif
 template <bool kCount, bool kProf, int kWidth, int kFeat, int kMode>
 __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A_param) {
     (void)A_param;   // read through ka (the same bytes: the kernarg segment holds A_param at offset 0)
@@ -367,7 +370,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             }
         }
     };
-    auto camera_finish = [&](bool starting, float cu_, float cv_, V3 disk) {
+    // seg: begin the segment here (else the caller does, RT_MERGE_SEG)
+    auto camera_finish = [&](bool starting, float cu_, float cv_, V3 disk, bool seg = true) {
         if (starting) {
             const CamView C = load_camera(lds_cam);
             V3 rd = scale(C.lens, disk);
@@ -386,7 +390,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             beta = mk(1, 1, 1);
             depth = 0;
             if (kCount) cnt.samples++;
-            begin_segment();
+            if (seg) begin_segment();
         }
     };
     // a path's radiance into its work item (de_nan, main.cpp:232-242; col += temp)
@@ -561,8 +565,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // |r.d| once per segment, for the media and the specular materials / sky
         const float dlen = (ready && A.need_dlen) ? len(r.d) : 0.f;
         const Recip rd = recip_of(dlen, ready && A.need_dlen);   // its reciprocal, for div_rn
-        Hit hr;
+        Hit hr;   // read only by lanes with a hit (shade_begin / shade_finish guard on `have`)
+#if !(RT_SHADE_LEAN & 2)
         hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
+#endif
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
             const int med_mat = kMedia ? media_hit<kCount, kInst>(A, lds_media, (LdsMediaConsts *)&lds_mconst, r, rd, g, have,
@@ -604,19 +610,25 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
         const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, jt, lane, cnt);
         mark(3);
+        // a scattered path and a new camera sample (disjoint lanes: a lane that started
+        // a sample this iteration was idle, not ready) begin their next segment in ONE
+        // place (RT_MERGE_SEG): the compiler otherwise materialises the segment state in
+        // both divergent branches
+        bool seg = false;
         if (ready && !ends) {
             const ShadeOut so = shade_finish(A, ready, have, r, rd, hr, st, pt, g);
             if (so.scattered) {
                 beta = mul(beta, so.att);
                 r = so.ray;
                 ++depth;
-                begin_segment();
+                if (RT_MERGE_SEG) seg = true; else begin_segment();
             } else {
                 end_path(mul(beta, so.emitted));
             }
         }
         mark(4);
-        camera_finish(starting, cu_, cv_, pt);
+        camera_finish(starting, cu_, cv_, pt, !RT_MERGE_SEG);
+        if (RT_MERGE_SEG && (seg || starting)) begin_segment();
         mark(3);
 #ifdef RT_PROBE_VALU
 #if RT_PROBE_VALU == 1
