@@ -429,7 +429,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
         {
             const bool starting = phase == PH_IDLE && !finished;
-            float cu_ = 0, cv_ = 0;
+            float cu_, cv_;   // set and read by starting lanes only
+#if !(RT_SHADE_LEAN & 8)
+            cu_ = 0; cv_ = 0;
+#endif
             camera_begin(starting, cu_, cv_);
             const V3 disk = coop_reject<2, kCount>(starting, g, slots, jt, lane, cnt, DiskCand());
             camera_finish(starting, cu_, cv_, disk);
@@ -605,7 +608,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (ends) end_path(mul(beta, shade_emitted(A, have, r, rd, st)));
         retire_and_claim();
         const bool starting = phase == PH_IDLE && !finished;
-        float cu_ = 0, cv_ = 0;
+        float cu_, cv_;   // set and read by starting lanes only
+#if !(RT_SHADE_LEAN & 8)
+            cu_ = 0; cv_ = 0;
+#endif
         camera_begin(starting, cu_, cv_);
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
         const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, jt, lane, cnt);
