@@ -17,7 +17,7 @@
 // (default copies kept alive across branches cost register moves; some of them, left
 // unset, made the allocator spill instead — those stay initialised):
 #ifndef RT_SHADE_LEAN
-#define RT_SHADE_LEAN 5   // bits: 1 scatter outputs, 2 hit record, 4 texture value, 8 jitter, 16 rejection points, 32 noise scale, 64 unit direction (2, 8: spills)
+#define RT_SHADE_LEAN 5   // bits: 1 scatter outputs, 2 hit record, 4 texture value, 8 jitter (2, 8: spills, off)
 #endif
 #define RT_INF __builtin_huge_valf()
 
@@ -986,10 +986,7 @@ __constant__ const CoopTable kCoop = CoopTable();
 template <int K, bool kCount, class Cand>
 __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, const LdsJump *jt, uint32_t lane,
                                           Counters &cnt, Cand cand) {
-    V3 res;   // read by the requesting lanes only, and each of them wins a point
-#if !(RT_SHADE_LEAN & 16)
-    res = mk(0, 0, 0);
-#endif
+    V3 res = mk(0, 0, 0);
     bool pending = want;
     uint64_t U = wballot(pending);
     while (U != 0ull) {
@@ -1041,10 +1038,7 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, co
 template <bool kCount>
 __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, CoopSlot *slots, const LdsJump *jt,
                                                 uint32_t lane, Counters &cnt) {
-    V3 res;   // read by the requesting lanes only, and each of them wins a point
-#if !(RT_SHADE_LEAN & 16)
-    res = mk(0, 0, 0);
-#endif
+    V3 res = mk(0, 0, 0);
     bool pending = want;
     const uint32_t K = disk ? 2u : 3u;
     uint64_t U = wballot(pending);
@@ -1560,10 +1554,7 @@ __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool re
     st.tv = mk(0, 0, 0);   // (lean: set for the textured and noisy lanes, the only readers)
 #endif
     bool noisy = false;
-    float nscale;   // read for the noisy lanes only
-#if !(RT_SHADE_LEAN & 32)
-    nscale = 0.f;
-#endif
+    float nscale = 0.f;
     if (shading) {
         if (kCount) cnt.shades++;
         st.kind = fbits(A.mats[hr.mat * 2 + 0].x);
@@ -1627,10 +1618,7 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
     // unit(r.d) (vec3.h:146) once, for the lanes whose scatter needs it (metal,
     // dielectric) instead of once in each of their branches
     const bool wants_unit = ready && have && st.live && (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC);
-    V3 ud;   // read by the metal and dielectric lanes only
-#if !(RT_SHADE_LEAN & 64)
-    ud = mk(0, 0, 0);
-#endif
+    V3 ud = mk(0, 0, 0);
     if (wants_unit) ud = mk(div_by(r.d.x, rd), div_by(r.d.y, rd), div_by(r.d.z, rd));
     if (!ready) return o;
     o.emitted = shade_emitted(A, have, r, rd, st);
