@@ -15,7 +15,7 @@ if [ -n "${TEST_LIB:-}" ]; then   # the parity tests again with a variant librar
       --timeout-method thread > gpurun_out/${TAG}_tests_lib.log 2>&1 || { echo "variant tests failed"; tail -30 gpurun_out/${TAG}_tests_lib.log; exit 1; }
   tail -1 gpurun_out/${TAG}_tests_lib.log
 fi
-C=variants/lean/librt_hip.so; A=variants/l53/librt_hip.so; B=variants/l117/librt_hip.so
+C=variants/lean/librt_hip.so; A=variants/preoff/librt_hip.so; B=variants/preon/librt_hip.so
 timeout -k 10 900 python3 tools/ab.py $C $A $B "$C@--config+c3" "$A@--config+c3" "$B@--config+c3" \
     "$C@--share-of+8" "$B@--share-of+8" "$C@--config+c2" "$B@--config+c2" --rounds 3 > gpurun_out/${TAG}.log 2>&1
 echo "ab rc=$?"; grep SUMMARY gpurun_out/${TAG}.log
