@@ -16,8 +16,13 @@
 // Values the shading stage and the samplers leave unset where no lane reads them
 // (default copies kept alive across branches cost register moves; some of them, left
 // unset, made the allocator spill instead — those stay initialised):
+// Such a value is FROZEN (unset_f: LLVM `freeze` of poison — an arbitrary but defined
+// value, so the compiler may pick whatever saves a move), never an uninitialised read:
+// reading an indeterminate value is undefined behaviour the compiler may exploit (round
+// 4's build with bits 16-64 left uninitialised faulted in the empty-scene case).
 #ifndef RT_SHADE_LEAN
-#define RT_SHADE_LEAN 5   // bits: 1 scatter outputs, 2 hit record, 4 texture value, 8 jitter (2, 8: spills, off)
+#define RT_SHADE_LEAN 117   // bits: 1 scatter outputs, 2 hit record, 4 texture value, 8 jitter, 16 rejection
+                            // points, 32 noise scale, 64 unit direction (2, 8: spills, off)
 #endif
 #define RT_INF __builtin_huge_valf()
 
@@ -30,6 +35,17 @@ __device__ __forceinline__ uint64_t wballot(bool b) { return __builtin_amdgcn_ba
 // ------------------------------------------------------------------ vec3
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 mk(float a, float b, float c) { V3 r; r.x = a; r.y = b; r.z = c; return r; }
+// a value no lane reads (RT_SHADE_LEAN): whatever the VGPR the register allocator gives
+// an empty asm's output holds — a defined value to the compiler (no undefined behaviour
+// to exploit), materialised by no instruction, so a join of it with a computed value
+// costs no move (LLVM's freeze, __builtin_nondeterministic_value, is folded to a
+// constant instead: 55 more v_movs in c4's variant than uninitialised values)
+__device__ __forceinline__ float unset_f() {
+    float x;
+    asm volatile("; unset %0" : "=v"(x));
+    return x;
+}
+__device__ __forceinline__ V3 unset_v3() { return mk(unset_f(), unset_f(), unset_f()); }
 __device__ __forceinline__ V3 add(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ V3 mul(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
@@ -986,7 +1002,8 @@ __constant__ const CoopTable kCoop = CoopTable();
 template <int K, bool kCount, class Cand>
 __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, const LdsJump *jt, uint32_t lane,
                                           Counters &cnt, Cand cand) {
-    V3 res = mk(0, 0, 0);
+    // read by the requesting lanes only, and each of them wins a point
+    V3 res = (RT_SHADE_LEAN & 16) ? unset_v3() : mk(0, 0, 0);
     bool pending = want;
     uint64_t U = wballot(pending);
     while (U != 0ull) {
@@ -1038,7 +1055,7 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, co
 template <bool kCount>
 __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, CoopSlot *slots, const LdsJump *jt,
                                                 uint32_t lane, Counters &cnt) {
-    V3 res = mk(0, 0, 0);
+    V3 res = (RT_SHADE_LEAN & 16) ? unset_v3() : mk(0, 0, 0);   // read by the requesting lanes only
     bool pending = want;
     const uint32_t K = disk ? 2u : 3u;
     uint64_t U = wballot(pending);
@@ -1550,11 +1567,9 @@ __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool re
     ShadeState st;
     st.kind = -1;
     st.live = false;
-#if !(RT_SHADE_LEAN & 4)
-    st.tv = mk(0, 0, 0);   // (lean: set for the textured and noisy lanes, the only readers)
-#endif
+    st.tv = (RT_SHADE_LEAN & 4) ? unset_v3() : mk(0, 0, 0);   // read for the textured and noisy lanes only
     bool noisy = false;
-    float nscale = 0.f;
+    float nscale = (RT_SHADE_LEAN & 32) ? unset_f() : 0.f;     // read for the noisy lanes only
     if (shading) {
         if (kCount) cnt.shades++;
         st.kind = fbits(A.mats[hr.mat * 2 + 0].x);
@@ -1606,11 +1621,17 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
                                                  const Hit &hr, const ShadeState &st, V3 rius, Rng &g) {
     ShadeOut o;
     o.scattered = false;
-#if !(RT_SHADE_LEAN & 1)
-    o.emitted = mk(0, 0, 0);   // (lean: set below for every ready lane, the only callers)
-    o.att = mk(0, 0, 0);
-    o.ray = r;
-#endif
+    // (lean: o.emitted is set below for every ready lane, the only callers; o.att and o.ray
+    // by the scattering branches)
+    if (RT_SHADE_LEAN & 1) {
+        o.emitted = unset_v3();
+        o.att = unset_v3();
+        o.ray.o = unset_v3(); o.ray.d = unset_v3(); o.ray.time = unset_f();
+    } else {
+        o.emitted = mk(0, 0, 0);
+        o.att = mk(0, 0, 0);
+        o.ray = r;
+    }
     // RT_SHADE_LEAN: o.att and o.ray are set by the scattering branches only (the caller
     // reads them only when o.scattered): default copies of the ray, kept alive down every
     // early return, were ~30 register moves per wave iteration
@@ -1618,18 +1639,15 @@ __device__ __forceinline__ ShadeOut shade_finish(const RtKernelArgs &A, bool rea
     // unit(r.d) (vec3.h:146) once, for the lanes whose scatter needs it (metal,
     // dielectric) instead of once in each of their branches
     const bool wants_unit = ready && have && st.live && (kind == RT_MAT_METAL || kind == RT_MAT_DIELECTRIC);
-    V3 ud = mk(0, 0, 0);
+    V3 ud = (RT_SHADE_LEAN & 64) ? unset_v3() : mk(0, 0, 0);   // read by the metal and dielectric lanes only
     if (wants_unit) ud = mk(div_by(r.d.x, rd), div_by(r.d.y, rd), div_by(r.d.z, rd));
     if (!ready) return o;
     o.emitted = shade_emitted(A, have, r, rd, st);
     if (!have || !st.live) return o;
     const float4 m0 = A.mats[hr.mat * 2 + 0];
     const float4 m1 = A.mats[hr.mat * 2 + 1];
-#if RT_SHADE_LEAN & 1
-    Ray ns;
-#else
     Ray ns = r;
-#endif
+    if (RT_SHADE_LEAN & 1) { ns.o = unset_v3(); ns.d = unset_v3(); ns.time = unset_f(); }
     if (kind == RT_MAT_LAMBERTIAN) {                              // material.h:64-69
         V3 target = add(add(hr.p, hr.n), rius);
         ns.o = hr.p; ns.d = sub(target, hr.p); ns.time = r.time;

@@ -429,10 +429,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
         {
             const bool starting = phase == PH_IDLE && !finished;
-            float cu_, cv_;   // set and read by starting lanes only
-#if !(RT_SHADE_LEAN & 8)
-            cu_ = 0; cv_ = 0;
-#endif
+            float cu_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f, cv_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f;   // starting lanes only
             camera_begin(starting, cu_, cv_);
             const V3 disk = coop_reject<2, kCount>(starting, g, slots, jt, lane, cnt, DiskCand());
             camera_finish(starting, cu_, cv_, disk);
@@ -569,9 +566,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         const float dlen = (ready && A.need_dlen) ? len(r.d) : 0.f;
         const Recip rd = recip_of(dlen, ready && A.need_dlen);   // its reciprocal, for div_rn
         Hit hr;   // read only by lanes with a hit (shade_begin / shade_finish guard on `have`)
-#if !(RT_SHADE_LEAN & 2)
-        hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
-#endif
+        if (RT_SHADE_LEAN & 2) {
+            hr.p = unset_v3(); hr.n = unset_v3(); hr.u = unset_f(); hr.v = unset_f(); hr.mat = 0;   // the index stays defined
+        } else {
+            hr.p = mk(0, 0, 0); hr.n = mk(0, 0, 0); hr.u = 0.f; hr.v = 0.f; hr.mat = 0;
+        }
         if (ready) {
             have = best_prim != 0xFFFFFFFFu;
             const int med_mat = kMedia ? media_hit<kCount, kInst>(A, lds_media, (LdsMediaConsts *)&lds_mconst, r, rd, g, have,
@@ -608,10 +607,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (ends) end_path(mul(beta, shade_emitted(A, have, r, rd, st)));
         retire_and_claim();
         const bool starting = phase == PH_IDLE && !finished;
-        float cu_, cv_;   // set and read by starting lanes only
-#if !(RT_SHADE_LEAN & 8)
-            cu_ = 0; cv_ = 0;
-#endif
+        float cu_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f, cv_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f;   // starting lanes only
         camera_begin(starting, cu_, cv_);
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
         const V3 pt = coop_reject_mixed<kCount>(st.wants_sphere || starting, starting, g, slots, jt, lane, cnt);

@@ -48,6 +48,10 @@ int upload(void **dst, const std::vector<T> &v) {
 // The scene's arrays share one device allocation filled by one copy (scene creation
 // was a dozen hipMalloc + hipMemcpy round trips): stage() appends an array to the
 // host image at a 256-B aligned offset, commit() uploads it and sets the pointers.
+// An empty array is staged as one zeroed 256-B sentinel: no scene pointer the kernel
+// receives is ever null, so a load the compiler speculates out of its branch (e.g. a
+// texture record read for lanes that have none) reads zeros instead of faulting on an
+// empty scene (edge_empty's illegal access).
 struct Arena {
     std::vector<uint8_t> host;
     std::vector<std::pair<void **, size_t>> fix;
@@ -55,10 +59,10 @@ struct Arena {
 template <class T>
 void stage(Arena &a, void **dst, const std::vector<T> &v) {
     *dst = nullptr;
-    if (v.empty()) return;
-    const size_t off = (a.host.size() + 255) & ~(size_t)255, bytes = v.size() * sizeof(T);
-    a.host.resize(off + bytes);
-    std::memcpy(a.host.data() + off, v.data(), bytes);
+    const size_t off = (a.host.size() + 255) & ~(size_t)255;
+    const size_t bytes = v.empty() ? std::max<size_t>(256, sizeof(T)) : v.size() * sizeof(T);
+    a.host.resize(off + bytes, 0);
+    if (!v.empty()) std::memcpy(a.host.data() + off, v.data(), bytes);
     a.fix.push_back({dst, off});
 }
 int commit(Arena &a, void **base) {
