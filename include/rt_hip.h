@@ -249,6 +249,12 @@ int rt_device_free(void *ptr);
 int rt_copy_to_host(void *dst, const void *src_dev, uint64_t bytes);
 int rt_device_count(int *out);
 
+/* Diagnostic: the device's float transcendentals of the path on n host inputs (out: n
+ * floats) — fn 0 the megakernel's sinf (texture.h:36, 55), 2 its asinf and 4 its
+ * atan2f(a, b) (hitable.h:15-16), all restated from glibc (rt_libm.h); 1, 3, 5 ocml's
+ * sinf / asinf / atan2f for comparison.  For the parity tests; not on the render path. */
+int rt_math_probe(int fn, const float *a, const float *b, float *out, int64_t n);
+
 /* ------------------------------------------------ multi-GPU
  * One process per GPU.  The root calls rt_dist_unique_id and hands the 128 bytes to
  * every rank (any side channel); each rank calls rt_dist_init (ncclCommInitRank),

@@ -9,6 +9,7 @@
 #include <type_traits>
 
 #include "rt_layout.h"
+#include "rt_libm.h"
 #include "rt_log_table.h"
 #include "rt_kernel.h"
 
@@ -25,6 +26,11 @@
                             // points, 32 noise scale, 64 unit direction (2, 8: spills, off)
 #endif
 #define RT_INF __builtin_huge_valf()
+// The float transcendentals of the path (texture sines, get_sphere_uv's atan2/asin) as
+// glibc computes them (rt_libm.h, exhaustively pinned); 0: ocml's (A/B, attribution)
+#ifndef RT_GLIBC_MATH
+#define RT_GLIBC_MATH 1
+#endif
 
 namespace {
 
@@ -206,10 +212,11 @@ struct Rng {
 // so next to 1 the result is r + r^2 p(r) with r = x - 1 exact: relatively accurate
 // without glibc's separate near-1 path (a branch nearly every wave took for some lane).
 // About 25 double operations instead of ocml's ~100.
-// c02 = 0.2, the polynomial's one coefficient that is neither an inline constant nor
-// folded: the megakernel passes it from LDS (read at the call), since as an immediate
-// the compiler kept it in two VGPRs across the whole persistent loop and spilled them.
-__host__ __device__ __forceinline__ double log_f64(double x, double c02 = 0.2) {
+// The polynomial's coefficients (none of them an inline constant) come in `pc`: the
+// megakernel passes them from LDS (read at the call), since as immediates the compiler
+// kept them in VGPRs across the whole persistent loop and spilled them.
+struct LogConsts { double c07, c06, c02, c025, c03; };   // the polynomial's coefficients
+__host__ __device__ __forceinline__ double log_f64(double x, LogConsts pc = LogConsts{1.0 / 7, -1.0 / 6, 0.2, -0.25, 1.0 / 3}) {
     if (!(x > 0.0)) return -__builtin_huge_val();
     uint64_t ix;
     __builtin_memcpy(&ix, &x, 8);
@@ -227,10 +234,10 @@ __host__ __device__ __forceinline__ double log_f64(double x, double c02 = 0.2) {
     const double hi = w + r;
     const double lo = (w - hi) + r + __builtin_fma(kd, ln2_lo, T[2]);
     const double r2 = r * r;
-    double q = __builtin_fma(r, 1.0 / 7, -1.0 / 6);
-    q = __builtin_fma(q, r, c02);
-    q = __builtin_fma(q, r, -0.25);
-    q = __builtin_fma(q, r, 1.0 / 3);
+    double q = __builtin_fma(r, pc.c07, pc.c06);
+    q = __builtin_fma(q, r, pc.c02);
+    q = __builtin_fma(q, r, pc.c025);
+    q = __builtin_fma(q, r, pc.c03);
     q = __builtin_fma(q, r, -0.5);
     const double p = r2 * q;
     return (lo + p) + hi;
@@ -438,8 +445,8 @@ struct Hit { V3 p, n; float u, v; int mat; };
 
 // get_sphere_uv (hitable.h:14-19): float atan2/asin, then the double M_PI arithmetic.
 __device__ __forceinline__ void sphere_uv(V3 p, float &u, float &v) {
-    const float phi = atan2f(p.z, p.x);
-    const float theta = asinf(p.y);
+    const float phi = RT_GLIBC_MATH ? rt_atan2f(p.z, p.x) : atan2f(p.z, p.x);
+    const float theta = RT_GLIBC_MATH ? rt_asinf(p.y) : asinf(p.y);
     u = (float)(1 - ((double)phi + 3.14159265358979323846) / (2 * 3.14159265358979323846));
     v = (float)(((double)theta + 3.14159265358979323846 / 2) / 3.14159265358979323846);
 }
@@ -585,7 +592,8 @@ __device__ __forceinline__ int tex_leaf(const RtKernelArgs &A, int ti, V3 p, flo
         t1 = A.texs[ti * 2 + 1];
         const int kind = fbits(t0.x);
         if (kind != RT_TEX_CHECKER) return kind;
-        float sines = sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+        float sines = RT_GLIBC_MATH ? rt_sinf(10 * p.x) * rt_sinf(10 * p.y) * rt_sinf(10 * p.z)
+                                    : sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
         ti = (sines < 0) ? fbits(t0.z) : fbits(t0.y);
     }
     return -1;
@@ -888,19 +896,15 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
 #ifndef RT_DESCEND_TAIL_DRY
 #define RT_DESCEND_TAIL_DRY 0
 #endif
-// kPark2 (the cooperative leaf tests, coop_leaves): a lane holding a parked leaf
-// parks a second one too when both together hold at most RT_MAX_LEAF primitives
-// (pleaf2), so a round's pair list is longer and rounds are fewer.
 // dry = true (a wave draining the launch's last paths, few lanes live): no tail cut —
 // the cut trades a few lanes' node steps for the others', and with a handful of lanes
 // every round's fixed cost (slab set-up, leaf pass, exit checks) is on the path's
 // latency, which is what the launch's end waits for.
-template <int kWidth, bool kCount, int kSteps = 1, bool kPark2 = false, class Nodes>
+template <int kWidth, bool kCount, int kSteps = 1, class Nodes>
 __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, const Slab &sl, float best_t,
-                                            uint32_t *stk, int &sp, Counters &cnt, uint32_t *pleaf2 = nullptr,
-                                            bool dry = false) {
+                                            uint32_t *stk, int &sp, Counters &cnt, bool dry = false) {
     const int kTail = dry ? RT_DESCEND_TAIL_DRY : (kSteps == 1 ? RT_DESCEND_TAIL : RT_DESCEND_TAIL2);
-    uint32_t pleaf = RT_EMPTY_CHILD, pl2 = RT_EMPTY_CHILD;
+    uint32_t pleaf = RT_EMPTY_CHILD;
     for (;;) {
 #pragma unroll
         for (int u = 0; u < kSteps; ++u) {
@@ -910,12 +914,6 @@ __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, 
             }
             const bool leaf = node != RT_EMPTY_CHILD && (node & RT_LEAF_BIT);
             const bool park = leaf && pleaf == RT_EMPTY_CHILD;
-            if (kPark2) {   // counts - 1 in bits 24..26: the two together hold <= 8 primitives
-                const bool park2 = leaf && !park && pl2 == RT_EMPTY_CHILD &&
-                                   ((pleaf >> 24) & 7u) + ((node >> 24) & 7u) <= (uint32_t)(RT_MAX_LEAF - 2);
-                pl2 = park2 ? node : pl2;
-                node = park2 ? RT_EMPTY_CHILD : node;
-            }
             pleaf = park ? node : pleaf;
             node = park ? RT_EMPTY_CHILD : node;
             const bool pop = node == RT_EMPTY_CHILD && sp > 0;
@@ -924,7 +922,6 @@ __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, 
             node = pop ? top : node;
         }
         if (__popcll(wballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD)) <= kTail) {
-            if (kPark2) *pleaf2 = pl2;
             return pleaf;
         }
     }
@@ -971,9 +968,6 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 // failed.  A lane loop that ran ~6 wave trips at ~16% SIMD efficiency (the
 // slowest lane of 48 decides) takes ~2-3 fully used trips.
 // Must be called with all 64 lanes of the wave active.
-#ifndef RT_COOP_STATS
-#define RT_COOP_STATS 0   // experiment: the count variant counts leaf rounds and their pairs in the rejection slots
-#endif
 struct CoopSlot {
     uint64_t ctr;
     uint64_t pad;
@@ -1020,7 +1014,7 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, co
         const uint64_t base = lcg_jump(slots[slot].ctr, jt[K * t]);   // the owner's state before candidate t
         V3 p;
         const uint64_t okm = wballot(cand(base, p));
-        if (kCount && !RT_COOP_STATS && first_active()) cnt.w_rius++;
+        if (kCount && first_active()) cnt.w_rius++;
         uint32_t src = lane;
         bool won = false;
         if (pending) {
@@ -1030,7 +1024,7 @@ __device__ __forceinline__ V3 coop_reject(bool want, Rng &g, CoopSlot *slots, co
             // candidates consumed: up to the winner, or all of the owner's this round
             const uint32_t tried = ((won ? src : 63u - r) * inv >> 16) + 1u;
             g.x = lcg_jump(g.x, jt[K * tried]);
-            if (kCount && !RT_COOP_STATS) cnt.l_rius += tried;
+            if (kCount) cnt.l_rius += tried;
             pending = !won;
         }
         // every lane takes part in the exchange (bpermute reads the source lane's register)
@@ -1075,7 +1069,7 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
         const float pz = kk == 3u ? 2.0f * (float)u48x(x3) - 1.0f : 0.0f;
         const V3 p = mk(2.0f * (float)u48x(x1) - 1.0f, 2.0f * (float)u48x(x2) - 1.0f, pz);
         const uint64_t okm = wballot((double)dot(p, p) < 1.0);
-        if (kCount && !RT_COOP_STATS && first_active()) cnt.w_rius++;
+        if (kCount && first_active()) cnt.w_rius++;
         uint32_t src = lane;
         bool won = false;
         if (pending) {
@@ -1084,7 +1078,7 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
             src = won ? (uint32_t)__builtin_ctzll(win) : lane;
             const uint32_t tried = ((won ? src : 63u - r) * inv >> 16) + 1u;
             g.x = lcg_jump(g.x, jt[K * tried]);
-            if (kCount && !RT_COOP_STATS) cnt.l_rius += tried;
+            if (kCount) cnt.l_rius += tried;
             pending = !won;
         }
         const float qx = __shfl(p.x, (int)src), qy = __shfl(p.y, (int)src), qz = __shfl(p.z, (int)src);
@@ -1175,145 +1169,14 @@ __device__ __forceinline__ CamView load_camera(const CamV4 *lds) {
 // hitable_list's acceptance (hitable_list.h:20-32: `t < closest`, ties to the earlier
 // list entry, the key) as selects: bitwise operators, so no short-circuit branches and
 // no exec-mask juggling around three moves per tested primitive.
-// kPacked (the LDS-BVH variants, < 2^15 primitives, RT_PACKED_BEST): best_prim holds
-// (key + 2^15) << 16 | primitive — the key's order in the high half, so one unsigned
-// compare decides a tie — and best_key is not used: one register and one select
-// fewer per test.  "Nothing found" is 0xFFFFFFFF, above every packed candidate.
-template <bool kPacked = false>
 __device__ __forceinline__ void keep_closest(bool in, float t, int key, uint32_t idx, float &best_t, int &best_key,
                                              uint32_t &best_prim) {
-    if constexpr (kPacked) {
-        const uint32_t kp = ((uint32_t)(key + 0x8000) << 16) | idx;
-        const bool take = in & ((t < best_t) | ((t == best_t) & (kp < best_prim)));
-        best_t = take ? t : best_t;
-        best_prim = take ? kp : best_prim;
-    } else {
-        const bool take = in & ((t < best_t) | ((t == best_t) & (key < best_key)));
-        best_t = take ? t : best_t;
-        best_key = take ? key : best_key;
-        best_prim = take ? idx : best_prim;
-    }
+    const bool take = in & ((t < best_t) | ((t == best_t) & (key < best_key)));
+    best_t = take ? t : best_t;
+    best_key = take ? key : best_key;
+    best_prim = take ? idx : best_prim;
 }
 
-// ------------------------------------------------------ cooperative leaf tests
-// A closest-hit candidate (t, key, primitive) as one u64 whose unsigned order is
-// keep_closest's: t first (its float bits mapped to an order-preserving uint, so
-// any t_min works; a miss, RT_INF, is never packed), then the list-order key
-// biased into 16 bits, then the primitive (keys are unique, so it never decides).
-// The LDS-BVH variant only: the host keeps those scenes below 2^15 primitives
-// (capi.cpp, RT_LDS_MAX_PRIMS).  "Nothing found" (best_prim = ~0) packs as an
-// all-ones low word, above every real key at the same t.
-__device__ __forceinline__ uint32_t ford(float t) {
-    const uint32_t b = __float_as_uint(t);
-    return b ^ ((uint32_t)((int32_t)b >> 31) | 0x80000000u);
-}
-__device__ __forceinline__ float fdeord(uint32_t u) {
-    return __uint_as_float(u ^ (((int32_t)u < 0) ? 0x80000000u : 0xFFFFFFFFu));
-}
-__device__ __forceinline__ uint64_t pack_hit(float t, int key, uint32_t prim) {
-    const uint32_t lo = ((uint32_t)(key + 0x8000) << 16) | (prim & 0xFFFFu);
-    return ((uint64_t)ford(t) << 32) | lo;
-}
-// The leaves the wave's lanes parked in this round (descend), tested by all 64
-// lanes at once instead of by each owner in turn (hitable_list.h:20-32 over the
-// leaf's primitives, bvh.h:29-54's leaf step).  Owner i's n_i primitives become
-// positions [o_i, o_i + n_i) of the wave's pair list (o = exclusive prefix sum of n,
-// from three ballots of n - 1's bits); lane L tests position 64 c + L in round c,
-// reading its owner's ray with ds_bpermute (the LDS crossbar, not VALU issue), and
-// folds its (t, key, primitive) into the owner's LDS word with ds_min_u64 — the
-// minimum of the owner's own closest hit so far and all candidates, i.e. exactly
-// the winner of keep_closest applied in any order.  The pair list costs one byte
-// per position: the owner's lane, written by every owner at [o_i, o_i + 8) from the
-// 8th byte down to the 1st, so a position's last write is its own owner's
-// (positions past T are never read; o_last + 7 <= 511 since the other 63 lanes
-// hold at most 504 primitives).  LDS: the wave's CoopSlot row (1 KiB), free
-// during traversal — bytes 0-511 the owner bytes, 512-1023 the 64 result words.
-// Must be called with all 64 lanes of the wave active.
-typedef __attribute__((address_space(3))) volatile uint8_t LdsVU8;
-typedef __attribute__((address_space(3))) uint8_t LdsU8;
-typedef __attribute__((address_space(3))) uint64_t LdsU64;
-__device__ __forceinline__ float bperm(uint32_t addr, float v) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute((int)addr, __float_as_int(v)));
-}
-// pleaf2: a second parked leaf (descend<kPark2>), its primitives at positions
-// [o_i + n_a, o_i + n_i) of the owner's range (the two hold <= 8 together).
-template <bool kCount, bool kInst, bool kPark2 = false>
-__device__ __forceinline__ void coop_leaves(uint32_t pleaf, uint32_t pleaf2, const Ray &r, const float4 *prims,
-                                            const float4 *insts, float tmin, CoopSlot *slots, uint32_t lane,
-                                            float &best_t, int &best_key, uint32_t &best_prim, Counters &cnt) {
-    const bool own = pleaf != RT_EMPTY_CHILD;
-    const uint64_t O = wballot(own);
-    if (O == 0ull) return;
-    const bool two = kPark2 && pleaf2 != RT_EMPTY_CHILD;
-    const uint32_t na = ((pleaf >> 24) & 7u) + 1u;
-    // count - 1 (RT_MAX_LEAF = 8)
-    const uint32_t c = own ? (two ? na + ((pleaf2 >> 24) & 7u) : na - 1u) : 0u;
-    const uint64_t b0 = wballot(c & 1u), b1 = wballot(c & 2u), b2 = wballot(c & 4u);
-    const uint32_t off = lanes_below(O) + lanes_below(b0) + 2u * lanes_below(b1) + 4u * lanes_below(b2);
-    const uint32_t T = (uint32_t)(__popcll(O) + __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
-    if (kCount && RT_COOP_STATS && first_active()) { cnt.w_rius++; cnt.l_rius += T; }   // experiment: rounds, pairs
-    LdsU8 *ob = (LdsU8 *)slots;
-    LdsU64 *res = (LdsU64 *)(ob + 512);
-    // primitive of position p: p + delta of its owner
-    const uint32_t delta = own ? RT_LEAF_FIRST(pleaf) - off : 0u;
-    // the second leaf's positions start at bnd; position p of it is primitive p + delta2
-    const uint32_t bnd = kPark2 ? off + na : 0u;
-    const uint32_t delta2 = two ? RT_LEAF_FIRST(pleaf2) - bnd : 0u;
-    if (own) {
-        LdsVU8 *w = (LdsVU8 *)(ob + off);
-#pragma unroll
-        for (int q = 7; q >= 0; --q) w[q] = (uint8_t)lane;   // volatile: 8 ordered byte stores
-        res[lane] = best_prim == 0xFFFFFFFFu ? ((uint64_t)ford(best_t) << 32) | 0xFFFFFFFFu
-                                             : pack_hit(best_t, best_key, best_prim);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t base = 0; base < T; base += 64) {   // wave-uniform
-        const uint32_t p = base + lane;
-        const bool act = p < T;
-        const uint32_t ow = act ? (uint32_t)((LdsVU8 *)ob)[p] : lane;
-        const uint32_t oa = ow << 2;
-        // every lane takes part in the exchange (a disabled source lane reads as 0): not
-        // inside the select's conditional operand
-        uint32_t od = (uint32_t)__builtin_amdgcn_ds_bpermute((int)oa, (int)delta);
-        if (kPark2) {
-            const uint32_t ob2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)oa, (int)bnd);
-            const uint32_t od2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)oa, (int)delta2);
-            od = p >= ob2 ? od2 : od;
-        }
-        const uint32_t idx = act ? p + od : 0u;
-        Ray q;
-        q.o = mk(bperm(oa, r.o.x), bperm(oa, r.o.y), bperm(oa, r.o.z));
-        q.d = mk(bperm(oa, r.d.x), bperm(oa, r.d.y), bperm(oa, r.d.z));
-        q.time = bperm(oa, r.time);
-        const float4 g0 = prims[idx * 4 + 0], mm = prims[idx * 4 + 1];
-        const bool rk = act && (fbits(mm.x) & 0xff) > RT_PRIM_MOVING_SPHERE;
-        const bool sk = act && !rk;
-        int key = 0, kind = 0;
-        float t;
-        // the kinds this round tests: a round of spheres only or of rects only runs that
-        // kind's test alone
-        if (wballot(rk) == 0ull) t = prim_t_head<kInst, 1>(g0, mm, prims, insts, idx, q, tmin, key, kind);
-        else if (wballot(sk) == 0ull) t = prim_t_head<kInst, 2>(g0, mm, prims, insts, idx, q, tmin, key, kind);
-        else t = prim_t_head<kInst, 3>(g0, mm, prims, insts, idx, q, tmin, key, kind);
-        if (kCount) { if (act) cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-        if (act && t != RT_INF) __atomic_fetch_min(&res[ow], pack_hit(t, key, idx), __ATOMIC_RELAXED);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (own) {
-        const uint64_t v = res[lane];
-        const uint32_t lo = (uint32_t)v;
-        best_t = fdeord((uint32_t)(v >> 32));
-        const bool none = lo == 0xFFFFFFFFu;
-        best_key = none ? 0x7FFFFFFF : (int)(lo >> 16) - 0x8000;
-        best_prim = none ? 0xFFFFFFFFu : (lo & 0xFFFFu);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 // Tests primitives [first, first + count) (4 float4 each, read through the scalar
 // cache: P is a constant-address-space pointer and q is uniform, so the records land
 // in SGPRs) against every lane's ray in lockstep: the primitive, its kind and its
@@ -1323,7 +1186,7 @@ __device__ __forceinline__ void coop_leaves(uint32_t pleaf, uint32_t pleaf2, con
 // instance chain; otherwise the caller transformed `r`.  Used by the BVH modes'
 // pre-scan; the flat scan, whose groups are ordered by kind, runs scan_group below.
 typedef __attribute__((address_space(4))) const F4v ConstF4;   // uniform index: scalar (SMEM) loads
-template <bool kCount, bool kInst, bool kPerPrimInst, bool kPacked = false, class PT>
+template <bool kCount, bool kInst, bool kPerPrimInst, class PT>
 __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const float4 *insts,
                                                const Ray &r, float tmin, bool in, int group_inst, float &best_t,
                                                int &best_key, uint32_t &best_prim, Counters &cnt) {
@@ -1346,7 +1209,7 @@ __device__ __forceinline__ void lockstep_prims(PT P, int first, int count, const
         const int key = kind <= RT_PRIM_MOVING_SPHERE ? order : -1 - order;
         if (kCount && in) cnt.prim(kind | (kInst && inst >= 0 ? 0x100 : 0));
         if (kCount && first_active()) cnt.w_prims++;
-        keep_closest<kPacked>(in, t, key, (uint32_t)q, best_t, best_key, best_prim);
+        keep_closest(in, t, key, (uint32_t)q, best_t, best_key, best_prim);
     }
 }
 
@@ -1424,7 +1287,7 @@ __device__ __forceinline__ void scan_group(const ConstF4 *P, int q, int kinds, i
 // Constants the media stage reads from LDS (rt_megakernel fills them at launch): a
 // volatile read at each use, so the compiler neither hoists them into registers held
 // across the persistent loop (where they were spilled to scratch) nor folds them back.
-struct MediaConsts { double c02; };   // log_f64's 0.2
+typedef LogConsts MediaConsts;   // log_f64's coefficients
 typedef __attribute__((address_space(3))) const volatile MediaConsts LdsMediaConsts;
 // constant_medium::hit for every medium after the surface search
 // (constant_medium.h:26-50): the boundary's entry/exit, clipped to [t_min, best]
@@ -1500,7 +1363,7 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     r1 = r1 < 0 ? 0.f : r1;
     const float distance_inside_boundary = (r2 - r1) * dlen;
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
-    const float hit_distance = (float)((double)neg_inv_density * log_f64(u48x(xk), mc->c02));
+    const float hit_distance = (float)((double)neg_inv_density * log_f64(u48x(xk), LogConsts{mc->c07, mc->c06, mc->c02, mc->c025, mc->c03}));
     const bool hit = ok && hit_distance < distance_inside_boundary;
     const float tm = r1 + div_by(hit_distance, rd);
     best_t = hit ? tm : best_t;
@@ -1587,7 +1450,7 @@ __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool re
     if (kCount && noisy) cnt.noise++;
     const float turb = coop_turb(noisy, scale(nscale, hr.p), A.ranvec, A.perm, slots, lane);   // perlin.h:64-74
     if (noisy) {                                                                               // texture.h:52-56
-        const float sv = 1 + sinf(nscale * hr.p.x + 5 * turb);
+        const float sv = 1 + (RT_GLIBC_MATH ? rt_sinf(nscale * hr.p.x + 5 * turb) : sinf(nscale * hr.p.x + 5 * turb));
         const float h = 0.5f * 1;
         st.tv = mk(sv * h, sv * h, sv * h);
     }

@@ -14,7 +14,6 @@
 #define RT_LDS_NODE_BYTES (4 * RT_LDS_NODE_CAP * 16)
 #define RT_LDS_STACK_BYTES(depth) ((RT_LDS_BLOCK / 64) * (depth) * 64 * 4)
 #define RT_LDS_BUDGET 163840   // LDS bytes per CU (160 KiB)
-#define RT_LDS_MAX_PRIMS 32767   // LDS variant: surface primitives (closest-hit key and index packed in 16 bits each)
 
 // scene features a megakernel variant carries code for (rt_launch_megakernel)
 #define RT_FEAT_INST 1      // translate / rotate_y / flip_normals chains
@@ -83,6 +82,7 @@ extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int 
 #define RT_RESOLVE_RAW 8      // write the sums themselves (checkpoints), not sum * k
 // floats per partial sum in the slab (3: rgb; RT_SLAB_F4=1 builds the 16-B layout, A/B only)
 extern "C" int rt_slab_floats(void);
+extern "C" hipError_t rt_launch_math_probe(int fn, const float *a, const float *b, float *out, int n, hipStream_t stream);
 extern "C" hipError_t rt_launch_resolve(const float *slab, uint32_t npix, int nchunks, float k, float4 *acc, int mode,
                                         const uint32_t *out_index, float *out, hipStream_t stream);
 // mode: 0 plain, 1 count, 2 profile; width: the scene's RtKernelArgs.bvh_width, 0: the flat-scan kernel

@@ -57,15 +57,6 @@ namespace {
 #define RT_DESCEND_STEPS 2
 #endif
 
-// Cooperative leaf tests in the LDS-BVH variant (rt_device.h coop_leaves); 0: each
-// lane tests its own parked leaf (A/B)
-#ifndef RT_COOP_LEAF
-#define RT_COOP_LEAF 0
-#endif
-// ... with a second parked leaf per lane (descend<kPark2>)
-#ifndef RT_COOP_PARK2
-#define RT_COOP_PARK2 0
-#endif
 
 // A wave whose claims found the pool dry and that holds at most this many live paths
 // runs latency-first (descend's tail cut off)
@@ -73,20 +64,16 @@ namespace {
 #define RT_DRY_LANES 16
 #endif
 
-// An item's radiance sum kept in its slab record instead of three registers held
-// across the persistent loop (end_path); 0: summed in registers, stored at retire
-#ifndef RT_SLAB_DIRECT
-#define RT_SLAB_DIRECT 0
-#endif
-
-// LDS-BVH variants: the closest hit's list-order key and primitive packed in one
-// register (rt_device.h keep_closest<kPacked>; capi.cpp keeps those scenes < 2^15 primitives)
-#ifndef RT_PACKED_BEST
-#define RT_PACKED_BEST 0
-#endif
 
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
+
+// Tail packing: once the pool is dry, a wave holding at most this many paths hands them
+// to another wave of its workgroup through LDS and retires (0: off)
+#ifndef RT_PACK_LANES
+#define RT_PACK_LANES 16
+#endif
+static_assert(RT_PACK_LANES <= 16, "a wave's packed paths fill its LDS rows at a stride of 16");
 
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
@@ -137,10 +124,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0,
                    kMedia = (kFeat & RT_FEAT_MEDIA) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
-    // the LDS-BVH2 variant tests its parked leaves with the whole wave (coop_leaves)
-    constexpr bool kCoopLeaf = RT_COOP_LEAF && kLds && kWidth == 2 && RT_LDS_SIGNED;
-    // the closest hit's key and primitive in one register (keep_closest<kPacked>)
-    constexpr bool kPacked = RT_PACKED_BEST && kLds && !kCoopLeaf;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
     __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : (kWidth >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH)][64];
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
@@ -151,6 +134,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // per wave: the next RT_PRE work items' sample starts, made 64 at a time (refill)
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
+    // tail packing: the workgroup's mailbox, (waves still running << 16) | the waves whose
+    // paths wait in their LDS rows, and each such wave's path count
+    __shared__ uint32_t lds_mail;
+    __shared__ uint32_t lds_pack_n[kBlock / 64];
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
@@ -165,9 +152,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     if (kMedia) load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) {
         store_camera(A, lds_cam);
-        lds_mconst.c02 = 0.2;
+        lds_mconst = LogConsts{1.0 / 7, -1.0 / 6, 0.2, -0.25, 1.0 / 3};
+        lds_mail = (uint32_t)(kBlock / 64) << 16;
     }
     for (uint32_t i = threadIdx.x; i < RT_LCG_JUMPS; i += kBlock) lds_jump[i] = kLcgJump.e[i];
+    rtl_lds_init(threadIdx.x);   // rt_libm.h's sine constants
     const LdsJump *jt = (const LdsJump *)lds_jump;
     if (kLds) {
         // interior child references become byte offsets into the planes (n * 16): a
@@ -314,12 +303,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // the next pre-made sample starts (one global atomic per A.claim items)
     auto retire_and_claim = [&]() {
         if (phase == PH_IDLE && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
-#if !RT_SLAB_DIRECT
             float *sl = A.slab + (size_t)item * RT_SLAB_FLOATS;   // 12 B per item (16 with RT_SLAB_F4)
             sl[0] = part.x;
             sl[1] = part.y;
             sl[2] = part.z;
-#endif
             item = 0xFFFFFFFFu;
         }
         bool need = phase == PH_IDLE && !finished && item == 0xFFFFFFFFu;
@@ -398,20 +385,105 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (!(L.x == L.x)) L.x = 0;
         if (!(L.y == L.y)) L.y = 0;
         if (!(L.z == L.z)) L.z = 0;
-#if RT_SLAB_DIRECT
-        // the item's sum lives in its slab record, not in registers across the loop: the
-        // first sample stores (0 + L == L bitwise: L >= +0 after de_nan), later samples of
-        // a multi-sample item add to what this lane stored (main.cpp:311's order)
-        float *sl = A.slab + (size_t)item * RT_SLAB_FLOATS;
-        if (A.chunk > 1 && (uint32_t)s_cur % (uint32_t)A.chunk != 0u) L = add(mk(sl[0], sl[1], sl[2]), L);
-        sl[0] = L.x;
-        sl[1] = L.y;
-        sl[2] = L.z;
-#else
         part = add(part, L);
-#endif
         ++s_cur;
         phase = PH_IDLE;
+    };
+
+    // ---- tail packing (RT_PACK_LANES) ---------------------------------------------
+    // Once the pool is dry, a wave holding at most RT_PACK_LANES paths writes them into its
+    // own LDS rows (its cooperative slots and sample-start slots, which nothing reads once
+    // it retires), publishes them in the workgroup's mailbox and retires; a dry wave with
+    // free lanes takes them in.  The launch's last paths then run in a few full waves
+    // instead of many nearly empty ones sharing each SIMD's issue.  A path moves with its
+    // item, sample range, depth, item sum, ray, throughput and drand48 states and restarts
+    // its segment's closest-hit search from the root (the hit does not depend on where the
+    // search started: the (t, key) order), so the image is bitwise unchanged.  The mailbox
+    // changes only by compare-and-swap: a wave retires — donating, or empty-handed — only
+    // while another wave still runs, and empty-handed only when no paths wait, so no path
+    // is ever stranded; every retirement removes a wave, so the exchange terminates.
+    constexpr bool kPack = RT_PACK_LANES > 0;
+    constexpr uint32_t kPackWords = kMedia ? 21u : 19u;
+    auto pack_row = [&](uint32_t w, uint32_t k) -> uint32_t * {   // dword k of wave w's paths, 16 paths a row
+        return k < 16u ? reinterpret_cast<uint32_t *>(lds_slots[w]) + k * 16u
+                       : reinterpret_cast<uint32_t *>(lds_pre_key[w]) + (k - 16u) * 16u;
+    };
+    auto pack_put = [&](uint32_t i) {   // this lane's path into its wave's rows, as path i
+        const uint32_t v[21] = {item, (uint32_t)s_cur, (uint32_t)s_end, (uint32_t)depth,
+                                __float_as_uint(part.x), __float_as_uint(part.y), __float_as_uint(part.z),
+                                __float_as_uint(r.o.x), __float_as_uint(r.o.y), __float_as_uint(r.o.z),
+                                __float_as_uint(r.d.x), __float_as_uint(r.d.y), __float_as_uint(r.d.z),
+                                __float_as_uint(r.time), __float_as_uint(beta.x), __float_as_uint(beta.y),
+                                __float_as_uint(beta.z), (uint32_t)g.x, (uint32_t)(g.x >> 32),
+                                (uint32_t)g.xm, (uint32_t)(g.xm >> 32)};
+#pragma unroll
+        for (uint32_t k = 0; k < kPackWords; ++k) pack_row(wave, k)[i] = v[k];
+    };
+    auto pack_get = [&](uint32_t d, uint32_t i) {   // path i of wave d into this lane
+        uint32_t v[21];
+#pragma unroll
+        for (uint32_t k = 0; k < kPackWords; ++k) v[k] = pack_row(d, k)[i];
+        item = v[0]; s_cur = (int)v[1]; s_end = (int)v[2]; depth = (int)v[3];
+        part = mk(__uint_as_float(v[4]), __uint_as_float(v[5]), __uint_as_float(v[6]));
+        r.o = mk(__uint_as_float(v[7]), __uint_as_float(v[8]), __uint_as_float(v[9]));
+        r.d = mk(__uint_as_float(v[10]), __uint_as_float(v[11]), __uint_as_float(v[12]));
+        r.time = __uint_as_float(v[13]);
+        beta = mk(__uint_as_float(v[14]), __uint_as_float(v[15]), __uint_as_float(v[16]));
+        g.x = ((uint64_t)v[18] << 32) | v[17];
+        if (kMedia) g.xm = ((uint64_t)v[20] << 32) | v[19];
+        finished = false;
+        pre_have = false;
+        begin_segment();
+        if (kCount) cnt.segments--;   // the donor counted this segment
+    };
+    typedef __attribute__((address_space(3))) uint32_t LdsU32;
+    auto mail_read = [&]() -> uint32_t {
+        return __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load((LdsU32 *)&lds_mail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    auto mail_cas = [&](uint32_t expect, uint32_t want) -> bool {   // one lane's compare-and-swap, the wave's verdict
+        int ok = 0;
+        if (first_active()) {
+            uint32_t e = expect;
+            ok = __hip_atomic_compare_exchange_strong((LdsU32 *)&lds_mail, &e, want, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+        }
+        return __builtin_amdgcn_readfirstlane(ok) != 0;
+    };
+    // A dry wave's exchange at the top of an iteration; true: the wave retires.
+    auto pack_exchange = [&](uint64_t &live) -> bool {
+        for (;;) {
+            const uint32_t w = mail_read();
+            const uint32_t alive = w >> 16, mask = w & 0xFFFFu;
+            const uint32_t nlive = (uint32_t)__popcll(live);
+            if (mask != 0u) {   // take the first waiting wave's paths if they fit the free lanes
+                const uint32_t d = (uint32_t)__builtin_ctz(mask);
+                const uint32_t n = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load((LdsU32 *)&lds_pack_n[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                if (n <= 64u - nlive) {
+                    if (!mail_cas(w, w & ~(1u << d))) continue;
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    const bool fr = finished;
+                    const uint32_t rk = lanes_below(wballot(fr));
+                    if (fr && rk < n) pack_get(d, rk);
+                    live = wballot(!finished);
+                    continue;
+                }
+            }
+            if (nlive == 0u) {   // nothing to run and (n <= 16 always fits) nothing waiting
+                if (mail_cas(w, w - (1u << 16))) return true;
+                continue;
+            }
+            if (nlive <= (uint32_t)RT_PACK_LANES && alive > 1u && wballot(!finished && phase != PH_TRAV) == 0ull) {
+                if (!finished) pack_put(lanes_below(live));
+                if (first_active())
+                    __hip_atomic_store((LdsU32 *)&lds_pack_n[wave], nlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (mail_cas(w, (w - (1u << 16)) | (1u << wave))) return true;
+                continue;
+            }
+            return false;
+        }
     };
 
     for (;;) {
@@ -423,7 +495,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // cooperative rounds: a metal's absorbed reflection; the others start their
         // next sample inside stage 5)
         retire_and_claim();
-        const uint64_t live = wballot(!finished);
+        uint64_t live = wballot(!finished);
+        if (kPack && exhausted && pre_count == 0) {
+            if (pack_exchange(live)) break;
+        }
         if (live == 0ull) break;
         // the pool is dry and few paths are left: the launch's end waits on their latency
         const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
@@ -482,44 +557,22 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             if (kPrescan && A.nprescan > 0) {
                 const bool fr = fresh && phase == PH_TRAV;
                 if (wballot(fr) != 0ull)
-                    lockstep_prims<kCount, kInst, true, kPacked>((const ConstF4 *)A.prims, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
+                    lockstep_prims<kCount, kInst, true>((const ConstF4 *)A.prims, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
                                                         best_t, best_key, best_prim, cnt);
                 fresh = false;
             }
             for (;;) {
                 if (wballot(phase == PH_TRAV) == 0ull) break;
                 if (__popcll(wballot(phase == PH_READY)) >= RT_READY_BATCH) break;
-                if constexpr (kCoopLeaf) {
-                    // descend, then the parked leaves tested by the whole wave (coop_leaves)
-                    const bool trav = phase == PH_TRAV;
-                    uint32_t pleaf = RT_EMPTY_CHILD, pleaf2 = RT_EMPTY_CHILD;
-                    if (trav) {
-                        Slab sl = make_slab(r, A.tmin);
-                        lnodes.prepare(sl);
-                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS, RT_COOP_PARK2>(lnodes, node, sl, best_t,
-                                                                                                  stk, sp, cnt, &pleaf2);
-                    }
-                    coop_leaves<kCount, kInst, RT_COOP_PARK2>(pleaf, pleaf2, r, A.prims, A.insts, A.tmin, slots, lane,
-                                                              best_t, best_key, best_prim, cnt);
-                    if (trav && node == RT_EMPTY_CHILD) phase = PH_READY;   // stack empty too (popped above)
-                } else if (phase == PH_TRAV) {
+                if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
                     Slab sl = make_slab(r, A.tmin);
                     uint32_t pleaf;
                     if constexpr (kLds && RT_LDS_SIGNED && kWidth == 2) lnodes.prepare(sl);
                     if constexpr (kLds)
-                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt,
-                                                                                      nullptr, dry);
+                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt, dry);
                     else
-                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt,
-                                                                                      nullptr, dry);
-                    if (kCount && RT_COOP_STATS) {   // experiment: leaf rounds and their primitives
-                        const uint64_t own = wballot(pleaf != RT_EMPTY_CHILD);
-                        const uint32_t n = pleaf != RT_EMPTY_CHILD ? RT_LEAF_COUNT(pleaf) : 0u;
-                        uint32_t sum = 0;
-                        for (int b = 0; b < 4; ++b) sum += (uint32_t)__popcll(wballot((n >> b) & 1u)) << b;
-                        if (own && first_active()) { cnt.w_rius++; cnt.l_rius += sum; }
-                    }
+                        pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt, dry);
                     if (pleaf != RT_EMPTY_CHILD) {
                         const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
                         // primitives in pairs: both 32-B heads are fetched before either test
@@ -534,11 +587,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                                 int key, kind;
                                 float t = prim_t_head<kInst, kK>(ga, ma, A.prims, A.insts, ia, r, A.tmin, key, kind);
                                 if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                                keep_closest<kPacked>(true, t, key, ia, best_t, best_key, best_prim);
+                                keep_closest(true, t, key, ia, best_t, best_key, best_prim);
                                 if (two) {
                                     t = prim_t_head<kInst, kK>(gb, mb, A.prims, A.insts, ib, r, A.tmin, key, kind);
                                     if (kCount) { cnt.prim(kind); if (first_active()) cnt.w_prims++; }
-                                    keep_closest<kPacked>(true, t, key, ib, best_t, best_key, best_prim);
+                                    keep_closest(true, t, key, ib, best_t, best_key, best_prim);
                                 }
                             };
                             // the kinds the wave tests in this pass: a wave of spheres only or of
@@ -581,7 +634,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 hr.n = mk(1, 0, 0);
                 hr.mat = med_mat;   // constant_medium.h:41-44 leaves u, v stale; no medium texture reads them
             } else if (have) {
-                hr = prim_record<kInst, kUV>(A.prims, A.insts, A.mats, kPacked ? best_prim & 0xFFFFu : best_prim, r, best_t);
+                hr = prim_record<kInst, kUV>(A.prims, A.insts, A.mats, best_prim, r, best_t);
             }
         }
 
@@ -665,7 +718,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         atomicMax(&T[2], (unsigned long long)(rt_exhaust ? rt_exhaust : rt_end));
         atomicMax(&T[3], ~rt_end);
         atomicMax(&T[4], rt_end);
-        atomicAdd(&T[5], rt_end);   // sum of the waves' ends: their mean, on the same clock as T[0..4]
+        // sum of the waves' lifetimes (end - own start: no overflow of absolute clock values
+        // summed over ~4,096 waves); the waves of a persistent grid start within µs of T[0]
+        atomicAdd(&T[5], rt_end - (unsigned long long)rt_start);
         atomicAdd(&T[6], 1ull);
         if (A.wave_log) {   // HW_ID (cu, simd, wave slot, se) and XCC_ID through s_getreg (reads)
             const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -733,7 +788,35 @@ __global__ __launch_bounds__(256) void rt_resolve(const float *__restrict__ slab
     out[3 * (size_t)o + 2] = col.z;
 }
 
+// Diagnostic (rt_math_probe): the device's float transcendentals on n inputs, for the
+// GPU tests to compare with glibc — fn 0 rt_sinf, 1 ocml sinf, 2 rt_asinf, 3 ocml asinf,
+// 4 rt_atan2f(a, b), 5 ocml atan2f(a, b) (rt_libm.h; the ocml forms are what the
+// megakernel used until round 5).
+__global__ __launch_bounds__(256) void rt_math_probe_kernel(int fn, const float *__restrict__ a,
+                                                            const float *__restrict__ b, float *__restrict__ out, int n) {
+    rtl_lds_init(threadIdx.x);
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = a[i];
+    float r;
+    switch (fn) {
+    case 0: r = rt_sinf(x); break;
+    case 1: r = sinf(x); break;
+    case 2: r = rt_asinf(x); break;
+    case 3: r = asinf(x); break;
+    case 4: r = rt_atan2f(x, b[i]); break;
+    default: r = atan2f(x, b[i]); break;
+    }
+    out[i] = r;
+}
+
 }  // namespace
+
+extern "C" hipError_t rt_launch_math_probe(int fn, const float *a, const float *b, float *out, int n, hipStream_t stream) {
+    hipLaunchKernelGGL(rt_math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, fn, a, b, out, n);
+    return hipGetLastError();
+}
 
 // --------------------------------------------------------------- launchers
 template <bool kCount, bool kProf, int kWidth, int kFeat, int kLds>
@@ -835,5 +918,5 @@ extern "C" int rt_megakernel_lds_static_actual(void) {
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 + 16 +
-                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8) + RT_LCG_JUMPS * 16) + 256;
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8) + RT_LCG_JUMPS * 16 + 4 + (RT_LDS_BLOCK / 64) * 4) + 256;
 }

@@ -1,0 +1,299 @@
+// rt_libm.h — the float transcendentals of the reference's hot path, restated so that the
+// device returns glibc 2.35's results BIT FOR BIT (the reference is built and run against
+// glibc's libm: SURVEY §8c; the oracle calls libm itself).
+//
+//   sinf    texture.h:36 (checker) and texture.h:55 (noise)
+//   asinf   hitable.h:16 (get_sphere_uv)
+//   atan2f  hitable.h:15 (get_sphere_uv)
+//
+// ocml's sinf / asinf / atan2f are accurate to ~1-2 ulp but round differently from glibc
+// now and then; one differing albedo bit makes the whole sample differ, which is what held
+// the full-spp crops at 0.82-0.88 bit-exact pixels.  These are glibc's
+// own algorithms, read from the x86-64 machine code of this image's libm.so.6 (constants
+// from its .rodata; no glibc source is vendored):
+//   * sinf: the double-precision sincosf scheme of glibc's s_sinf.c (quadrant reduction by
+//     one multiply-subtract for |x| < 120, by 4/pi to 192 bits above; degree-7 sine and
+//     degree-8 cosine polynomials in double), as the FMA ifunc variant glibc selects on an
+//     FMA-capable x86-64 host: the multiply-adds below are fused exactly where that build
+//     fuses them;
+//   * asinf, atan2f / atanf: the fdlibm-derived float code of glibc's e_asinf.c, e_atan2f.c
+//     and s_atanf.c (no ifunc variants: plain float arithmetic, no FMA).
+// Pinned exhaustively on the host (tools/libm_exhaustive.c, profiles/r05/libm_exhaustive.log):
+// every one of the 2^32 - 2^24 finite floats for sinf, asinf and atanf, and 4e9 (y, x)
+// pairs for atan2f, against glibc — zero differences.  tests/test_host_api.py re-checks a
+// strided subset on every CPU run; tests/test_gpu_parity.py checks the device results.
+//
+// Compiled as device code (rt_device.h) and as plain C/C++ on the host (the checks):
+// -ffp-contract=off everywhere, explicit fma where glibc's build fused.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#define RT_LIBM_FN __host__ __device__ __forceinline__
+#ifndef RTL_LARGE_FN
+#define RTL_LARGE_FN __host__ __device__ __forceinline__
+#endif
+#ifndef RTL_SINF_FN
+#define RTL_SINF_FN __host__ __device__ __forceinline__
+#endif
+#else
+#define RT_LIBM_FN static inline
+#define RTL_LARGE_FN static inline
+#define RTL_SINF_FN static inline
+#endif
+
+// The sine's double constants on the device: read from a workgroup LDS copy (volatile:
+// at each use) that the megakernel fills at launch (rtl_lds_init).  As immediates the
+// compiler hoisted them out of the persistent loop into registers held across it, which
+// spilled them and the media stage's log constants (c4's variant: 44 B of scratch).
+enum { RTL_K_S1, RTL_K_S2, RTL_K_S3, RTL_K_C0, RTL_K_C1, RTL_K_C2, RTL_K_C3, RTL_K_C4, RTL_K_HPI_INV, RTL_K_HPI,
+       RTL_K_PI63, RTL_K_N };
+#if defined(__HIPCC__)
+__shared__ double rtl_lds_k[RTL_K_N];
+__device__ __forceinline__ void rtl_lds_init(unsigned tid) {
+    const double k[RTL_K_N] = {-0x1.555545995a603p-3, 0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13, 0x1p0,
+                               -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10,
+                               0x1.99343027bf8c3p-16, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+                               0x1.921FB54442D18p-62};
+    if (tid < RTL_K_N) rtl_lds_k[tid] = k[tid];
+}
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define rtl_k(i, v) (((__attribute__((address_space(3))) const volatile double *)rtl_lds_k)[i])
+#else
+#define rtl_k(i, v) (v)
+#endif
+
+RT_LIBM_FN uint32_t rtl_asu(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+RT_LIBM_FN float rtl_asf(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+// ---------------------------------------------------------------- sinf (s_sinf.c)
+// libm's __sincosf_table[2] holds, per table: the sign per quadrant {1, -1, -1, 1},
+// 2/pi * 2^24 (0x1.45f306dc9c883p+23), pi/2 (0x1.921fb54442d18p+0) and the coefficients
+// below; table 1 (quadrants 2 and 3) is table 0 with the cosine coefficients negated.
+// Held as immediates here (the table index is per lane): `neg` selects table 1's.
+#define RTL_HPI_INV 0x1.45f306dc9c883p+23
+#define RTL_HPI 0x1.921fb54442d18p+0
+#define RTL_S1 (-0x1.555545995a603p-3)
+#define RTL_S2 0x1.1107605230bc4p-7
+#define RTL_S3 (-0x1.994eb3774cf24p-13)
+#define RTL_C0 0x1p0
+#define RTL_C1 (-0x1.ffffffd0c621cp-2)
+#define RTL_C2 0x1.55553e1068f19p-5
+#define RTL_C3 (-0x1.6c087e89a359dp-10)
+#define RTL_C4 0x1.99343027bf8c3p-16
+// __inv_pio4: 4/pi, 8 new bits per entry
+#if defined(__HIPCC__)
+__constant__
+#endif
+static const uint32_t rtl_inv_pio4[24] = {
+    0xa2,       0xa2f9,     0xa2f983,   0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+    0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
+    0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041};
+
+RT_LIBM_FN uint32_t rtl_abstop12(float f) { return (rtl_asu(f) >> 20) & 0x7ff; }
+
+// sinf_poly: odd quadrant -> the cosine polynomial (table 1's coefficients when neg)
+RT_LIBM_FN float rtl_sinf_poly(double x, double x2, int n, int neg) {
+    if ((n & 1) == 0) {
+        const double x3 = x * x2;
+        const double s1 = fma(x2, rtl_k(RTL_K_S3, RTL_S3), rtl_k(RTL_K_S2, RTL_S2));
+        const double x7 = x3 * x2;
+        const double s = fma(x3, rtl_k(RTL_K_S1, RTL_S1), x);
+        return (float)fma(x7, s1, s);
+    }
+    const double c0 = rtl_k(RTL_K_C0, RTL_C0), c1k = rtl_k(RTL_K_C1, RTL_C1), c2k = rtl_k(RTL_K_C2, RTL_C2),
+                 c3k = rtl_k(RTL_K_C3, RTL_C3), c4k = rtl_k(RTL_K_C4, RTL_C4);
+    const double k0 = neg ? -c0 : c0, k1 = neg ? -c1k : c1k, k2 = neg ? -c2k : c2k, k3 = neg ? -c3k : c3k,
+                 k4 = neg ? -c4k : c4k;
+    const double x4 = x2 * x2;
+    const double c2 = fma(x2, k4, k3);
+    const double c1 = fma(x2, k1, k0);
+    const double x6 = x4 * x2;
+    const double c = fma(x4, k2, c1);
+    return (float)fma(x6, c2, c);
+}
+
+// |x| < 120: x - n pi/2 by one fused multiply-subtract; n from the 2^24-scaled quotient
+RT_LIBM_FN double rtl_reduce_fast(double x, int *np) {
+    const double r = x * rtl_k(RTL_K_HPI_INV, RTL_HPI_INV);
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return fma(-(double)n, rtl_k(RTL_K_HPI, RTL_HPI), x);
+}
+
+// |x| >= 120: x * 4/pi with 4/pi to 192 bits, in integers
+RTL_LARGE_FN double rtl_reduce_large(uint32_t xi, int *np) {
+    const uint32_t *arr = &rtl_inv_pio4[(xi >> 26) & 15];
+    const int shift = (xi >> 23) & 7;
+    xi = (xi & 0xffffff) | 0x800000;
+    xi <<= shift;
+    uint64_t res0 = xi * arr[0];
+    const uint64_t res1 = (uint64_t)xi * arr[4];
+    const uint64_t res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    const uint64_t n = (res0 + (1ULL << 61)) >> 62;
+    res0 -= n << 62;
+    const double x = (double)(int64_t)res0;
+    *np = (int)n;
+    return x * rtl_k(RTL_K_PI63, 0x1.921FB54442D18p-62);
+}
+
+RTL_SINF_FN float rt_sinf(float y) {
+    double x = y;
+    int n;
+    if (rtl_abstop12(y) < rtl_abstop12(0x1.921FB6p-1f)) {   // |y| < pi/4
+        if (rtl_abstop12(y) < rtl_abstop12(0x1p-12f)) return y;
+        return rtl_sinf_poly(x, x * x, 0, 0);
+    }
+    if (rtl_abstop12(y) < rtl_abstop12(120.0f)) {
+        x = rtl_reduce_fast(x, &n);
+        const double s = ((n + 1) & 2) ? -1.0 : 1.0;   // sign[n & 3] = {1, -1, -1, 1}
+        return rtl_sinf_poly(x * s, x * x, n, n & 2);
+    }
+    if (rtl_abstop12(y) < rtl_abstop12(__builtin_inff())) {
+        const uint32_t xi = rtl_asu(y);
+        const int sign = (int)(xi >> 31);
+        x = rtl_reduce_large(xi, &n);
+        const double s = ((n + sign + 1) & 2) ? -1.0 : 1.0;
+        return rtl_sinf_poly(x * s, x * x, n, (n + sign) & 2);
+    }
+    return (y - y) / (y - y);   // inf or NaN: NaN
+}
+
+// ------------------------------------------------------------- asinf (e_asinf.c)
+RT_LIBM_FN float rt_asinf(float x) {
+    const float one = 1.0f, huge = rtl_asf(0x7149f2ca);
+    const float pio2_hi = rtl_asf(0x3fc90fdb), pio2_lo = rtl_asf(0xb33bbd2e), pio4_hi = rtl_asf(0x3f490fdb);
+    const float p0 = rtl_asf(0x3e2aaae4), p1 = rtl_asf(0x3d9980f2), p2 = rtl_asf(0x3d3a3f25),
+                p3 = rtl_asf(0x3cc6141e), p4 = rtl_asf(0x3d2cb694);
+    const int32_t hx = (int32_t)rtl_asu(x);
+    const int32_t ix = hx & 0x7fffffff;
+    float t, w, p, q, c, r, s;
+    if (ix == 0x3f800000) return x * pio2_hi + x * pio2_lo;   // asin(+-1) = +-pi/2
+    if (ix > 0x3f800000) return (x - x) / (x - x);           // |x| > 1: NaN
+    if (ix < 0x3f000000) {                                   // |x| < 0.5
+        if (ix < 0x32000000) {
+            if (huge + x > one) return x;
+        } else {
+            t = x * x;
+            w = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+            return x + x * w;
+        }
+    }
+    // 1 > |x| >= 0.5
+    w = one - fabsf(x);
+    t = w * 0.5f;
+    p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+    s = sqrtf(t);
+    if (ix >= 0x3F79999A) {   // |x| > 0.975
+        t = pio2_hi - (2.0f * (s + s * p) - pio2_lo);
+    } else {
+        w = rtl_asf(rtl_asu(s) & 0xfffff000u);
+        c = (t - w * w) / (s + w);
+        r = p;
+        p = 2.0f * s * r - (pio2_lo - 2.0f * c);
+        q = pio4_hi - 2.0f * w;
+        t = pio4_hi - (p - q);
+    }
+    return hx > 0 ? t : -t;
+}
+
+// -------------------------------------------------------------- atanf (s_atanf.c)
+RT_LIBM_FN float rt_atanf(float x) {
+    const float atanhi[4] = {rtl_asf(0x3eed6338), rtl_asf(0x3f490fda), rtl_asf(0x3f7b985e), rtl_asf(0x3fc90fda)};
+    const float atanlo[4] = {rtl_asf(0x31ac3769), rtl_asf(0x33222168), rtl_asf(0x33140fb4), rtl_asf(0x33a22168)};
+    const float aT0 = rtl_asf(0x3eaaaaab), aT1 = rtl_asf(0xbe4ccccd), aT2 = rtl_asf(0x3e124925),
+                aT3 = rtl_asf(0xbde38e38), aT4 = rtl_asf(0x3dba2e6e), aT5 = rtl_asf(0xbd9d8795),
+                aT6 = rtl_asf(0x3d886b35), aT7 = rtl_asf(0xbd6ef16b), aT8 = rtl_asf(0x3d4bda59),
+                aT9 = rtl_asf(0xbd15a221), aT10 = rtl_asf(0x3c8569d7);
+    const float one = 1.0f, huge = rtl_asf(0x7149f2ca);
+    const int32_t hx = (int32_t)rtl_asu(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {   // |x| >= 2^25
+        if (ix > 0x7f800000) return x + x;   // NaN
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3ee00000) {    // |x| < 0.4375
+        if (ix < 0x31000000) {   // |x| < 2^-29
+            if (huge + x > one) return x;
+        }
+        id = -1;
+    } else {
+        x = fabsf(x);
+        if (ix < 0x3f980000) {      // |x| < 1.1875
+            if (ix < 0x3f300000) {  // 7/16 <= |x| < 11/16
+                id = 0;
+                x = (2.0f * x - one) / (2.0f + x);
+            } else {                // 11/16 <= |x| < 19/16
+                id = 1;
+                x = (x - one) / (x + one);
+            }
+        } else if (ix < 0x401c0000) {   // |x| < 2.4375
+            id = 2;
+            x = (x - 1.5f) / (one + 1.5f * x);
+        } else {                        // 2.4375 <= |x| < 2^25
+            id = 3;
+            x = -1.0f / x;
+        }
+    }
+    const float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -zz : zz;
+}
+
+// ----------------------------------------------------------- atan2f (e_atan2f.c)
+RT_LIBM_FN float rt_atan2f(float y, float x) {
+    const float tiny = rtl_asf(0x0da24260), pi_o_4 = rtl_asf(0x3f490fdb), pi_o_2 = rtl_asf(0x3fc90fdb),
+                pi = rtl_asf(0x40490fdb), pi_lo = rtl_asf(0xb3bbbd2e);
+    const int32_t hx = (int32_t)rtl_asu(x), hy = (int32_t)rtl_asu(y);
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    float z;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;   // NaN
+    if (hx == 0x3f800000) return rt_atanf(y);               // x = 1.0
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);      // 2 * sign(x) + sign(y)
+    if (iy == 0) {   // y = 0
+        switch (m) {
+        case 0:
+        case 1: return y;
+        case 2: return pi + tiny;
+        default: return -pi - tiny;
+        }
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;   // x = 0
+    if (ix == 0x7f800000) {   // x = INF
+        if (iy == 0x7f800000) {
+            switch (m) {
+            case 0: return pi_o_4 + tiny;
+            case 1: return -pi_o_4 - tiny;
+            case 2: return 3.0f * pi_o_4 + tiny;
+            default: return -3.0f * pi_o_4 - tiny;
+            }
+        }
+        switch (m) {
+        case 0: return 0.0f;
+        case 1: return -0.0f;
+        case 2: return pi + tiny;
+        default: return -pi - tiny;
+        }
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;   // y = INF
+    const int32_t k = (iy - ix) >> 23;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;   // |y / x| > 2^60
+    else if (hx < 0 && k < -60) z = 0.0f;    // |y| / x < -2^60
+    else z = rt_atanf(fabsf(y / x));
+    switch (m) {
+    case 0: return z;
+    case 1: return rtl_asf(rtl_asu(z) ^ 0x80000000u);
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+    }
+}

@@ -206,6 +206,22 @@ int rt_copy_to_host(void *dst, const void *src, uint64_t bytes) {
     return RT_OK;
 }
 
+int rt_math_probe(int fn, const float *a, const float *b, float *out, int64_t n) {
+    if (fn < 0 || fn > 5 || n < 0 || n > (1 << 30) || (n && (!a || !out || (fn >= 4 && !b))))
+        return fail(RT_ERR_INVALID, "rt_math_probe: bad arguments");
+    if (n == 0) return RT_OK;
+    const size_t bytes = (size_t)n * sizeof(float);
+    float *d = nullptr;
+    HIP_TRY(hipMalloc((void **)&d, 3 * bytes));
+    hipError_t e = hipMemcpy(d, a, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && fn >= 4) e = hipMemcpy(d + n, b, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rt_launch_math_probe(fn, d, d + n, d + 2 * n, (int)n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 2 * n, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return hip_fail(e, "rt_math_probe");
+    return RT_OK;
+}
+
 int rt_camera_init(rt_camera_desc *out, const float lookfrom[3], const float lookat[3], const float vup[3], float vfov,
                    float aspect, float aperture, float focus_dist, float t0, float t1) {
     if (!out || !lookfrom || !lookat || !vup) return fail(RT_ERR_INVALID, "rt_camera_init: null argument");
@@ -574,10 +590,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             lds_cu = 0;
         const long stat = std::max<long>(rt_megakernel_lds_static_bytes(), rt_megakernel_lds_static_actual());
         const long need_actual = need - rt_megakernel_lds_static_bytes() + stat;
-        // (it carries the closest hit's list-order key and primitive index in 16 bits
-        // each, rt_device.h keep_closest<kPacked> / pack_hit: fewer than RT_LDS_MAX_PRIMS)
         s->lds_nodes = want && !s->scan && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
-                       s->nnodes <= RT_LDS_NODE_CAP && d->nprims < RT_LDS_MAX_PRIMS &&
+                       s->nnodes <= RT_LDS_NODE_CAP &&
                        need_actual <= std::min<long>(RT_LDS_BUDGET, lds_cu);
         if (s->lds_nodes)
             for (int mode = 0; mode < 3; mode++) s->grid[mode] = s->cus;
@@ -885,7 +899,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->wave_exhaust_last_us = ((double)T[2] - t0) * us;
             stats->wave_end_first_us = ((double)~T[3] - t0) * us;
             stats->wave_end_last_us = ((double)T[4] - t0) * us;
-            stats->wave_end_mean_us = T[6] ? ((double)T[5] / (double)T[6] - t0) * us : 0.0;   // T[5]: sum of ends
+            stats->wave_end_mean_us = T[6] ? (double)T[5] / (double)T[6] * us : 0.0;   // T[5]: sum of lifetimes
         }
         stats->grid = (double)s->grid[mode];
         stats->lds_level = s->lds_nodes ? 1.0 : 0.0;

@@ -156,15 +156,33 @@ def lib():
                                                ctypes.c_void_p]),
             "rt_dist_render": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, P(RtCameraDesc), P(RtRenderParams),
                                               ctypes.c_void_p, P(RtStats)]),
+            "rt_math_probe": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_int64]),
             "rt_last_error": (ctypes.c_char_p, []),
             "rt_version": (ctypes.c_char_p, []),
         }
+        optional = {"rt_math_probe"}   # diagnostics a library built before them lacks (A/B variants)
         for name, (res, args) in sig.items():
+            if name in optional and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+MATH_PROBE = {"sinf": 0, "sinf_ocml": 1, "asinf": 2, "asinf_ocml": 3, "atan2f": 4, "atan2f_ocml": 5}
+
+
+def math_probe(fn: str, a: np.ndarray, b: np.ndarray | None = None) -> np.ndarray:
+    """The device's float transcendentals on host inputs (rt_math_probe): `fn` one of
+    MATH_PROBE (the megakernel's glibc restatements, rt_libm.h, or ocml's forms)."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    bb = np.ascontiguousarray(b if b is not None else np.zeros_like(a), dtype=np.float32)
+    out = np.empty_like(a)
+    _check(lib().rt_math_probe(MATH_PROBE[fn], a.ctypes.data, bb.ctypes.data, out.ctypes.data, a.size))
+    return out
 
 
 def _check(rc):

@@ -160,6 +160,21 @@ def test_device_log_matches_glibc(tmp_path):
     assert fdiff == 0
 
 
+def test_libm_restatement_matches_glibc(tmp_path):
+    """csrc/hip/rt_libm.h (the device's sinf / asinf / atan2f, restated from glibc) against
+    this host's glibc: every 4,099th finite float and 10^6 atan2f pairs bitwise (the
+    exhaustive run over all 2^32 - 2^24 finite floats: profiles/r05/libm_exhaustive.log)."""
+    import subprocess
+    pkg = os.path.dirname(rtnw.LIB_PATH)
+    exe = str(tmp_path / "libm_check")
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", "-I", os.path.join(pkg, "csrc", "hip"),
+                    os.path.join(ROOT, "tools", "libm_exhaustive.c"), "-o", exe, "-lm"], check=True, capture_output=True)
+    out = subprocess.run([exe, "4099", "1000000"], capture_output=True, text=True)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout
+    assert "sinf   1043716 finite floats, 0 differ" in out.stdout and "atan2f 1000000 pairs, 0 differ" in out.stdout
+
+
 def test_bvh_builder_invariants(tmp_path):
     """tests/native/bvh_check.cpp: for BVH widths 2, 4, 8 and compressed 8, on every built-in scene and on
     adversarial synthetic ones (200k uniform, 50k identical, 20k geometric spheres):

@@ -27,7 +27,7 @@ for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:l2" 
   timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/pmc_$name -o run --output-format csv -- $B > $O/pmc_$name.log 2>&1
 done
 echo "== pmc lanes"   # VALU lane utilisation (tools/lanes_summary.py reads gpurun_out/lanes_<cfg>)
-timeout -s KILL 240 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d gpurun_out/lanes_$CFG -o run \
+timeout -s KILL 240 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU -d gpurun_out/lanes_$CFG -o run \
     --output-format csv -- $B > $O/pmc_lanes.log 2>&1
 i=0
 for ctrs in "SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT" \

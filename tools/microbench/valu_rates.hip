@@ -32,6 +32,43 @@ __device__ unsigned long long g_stamps[4];
         out[blockIdx.x * 256 + threadIdx.x] = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;        \
         STAMP(2)                                                                            \
     }
+// K32D: the instruction reads two more VGPRs, distinct (c and d): the VOP3 forms' issue cost
+// without a source register read twice
+#define K32D(name, asmtxt)                                                                  \
+    __global__ __launch_bounds__(256) void name(uint32_t *out, uint32_t c) {                \
+        STAMP(0)                                                                            \
+        uint32_t x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4,      \
+                 x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;                                     \
+        const uint32_t d = c ^ threadIdx.x;                                                 \
+        for (int i = 0; i < N_ITER; ++i) {                                                  \
+            _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                 \
+                BODY8(STEPD)                                                                \
+            }                                                                               \
+        }                                                                                   \
+        out[blockIdx.x * 256 + threadIdx.x] = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;        \
+        STAMP(2)                                                                            \
+    }
+#define STEPD(x) asm volatile(ASM : "+v"(x) : "v"(c), "v"(d));
+#define ASM "v_fma_f32 %0, %0, %1, %2"
+K32D(k_fma_f32_d, ASM)
+#undef ASM
+#define ASM "v_min3_f32 %0, %0, %1, %2"
+K32D(k_min3_f32_d, ASM)
+#undef ASM
+#define ASM "v_med3_f32 %0, %0, %1, %2"
+K32D(k_med3_f32_d, ASM)
+#undef ASM
+#define ASM "v_add3_u32 %0, %0, %1, %2"
+K32D(k_add3_u32_d, ASM)
+#undef ASM
+#define ASM "v_cndmask_b32_e64 %0, %1, %2, s[40:41]"
+K32D(k_cndmask_s_d, ASM)
+#undef ASM
+#define ASM "v_mad_u32_u24 %0, %0, %1, %2"
+K32D(k_mad_u32_u24_d, ASM)
+#undef ASM
+#undef STEPD
+
 #define STEP(x) asm volatile(ASM : "+v"(x) : "v"(c));
 #define ASM "v_add_u32 %0, %0, %1"
 K32(k_add_u32, ASM)
@@ -69,15 +106,13 @@ K32(k_max_f32, ASM)
 #define ASM "v_min3_f32 %0, %0, %1, %0"
 K32(k_min3_f32, ASM)
 #undef ASM
-#define ASM "v_cndmask_b32 %0, %0, %1, vcc"
-K32(k_cndmask, ASM)
-#undef ASM
+// (the VCC-mask form: k_cndmask_vcc below, with VCC bound as an operand; written as a
+// plain K32 kernel it read a VCC the compiler also used, and measured 23 cycles)
 #define ASM "v_mov_b32 %0, %1"
 K32(k_mov_b32, ASM)
 #undef ASM
-#define ASM "v_cmp_lt_f32 vcc, %0, %1"
-K32(k_cmp_f32, ASM)
-#undef ASM
+// (v_cmp_lt_f32 writing VCC: k_cmp_f32 below, with VCC declared clobbered; as a plain K32
+// kernel it overwrote the clock stamp the compiler kept in VCC: "measured clock 100 MHz")
 #define ASM "v_sqrt_f32 %0, %0"
 K32(k_sqrt_f32, ASM)
 #undef ASM
@@ -173,6 +208,47 @@ K64(k_mov_b64, ASM)
 #undef ASM
 #undef STEP
 
+// compares write VCC (declared clobbered): 8 independent compares of the chains' values
+__global__ __launch_bounds__(256) void k_cmp_f32(uint32_t *out, uint32_t c) {
+    STAMP(0)
+    float x[8];
+    for (int j = 0; j < 8; ++j) x[j] = (float)(threadIdx.x + j);
+    const float cf = (float)c;
+    for (int i = 0; i < N_ITER; ++i) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) asm volatile("v_cmp_lt_f32 vcc, %0, %1" : : "v"(x[j]), "v"(cf) : "vcc");
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = (uint32_t)x[threadIdx.x & 7];
+    STAMP(2)
+}
+// the VCC-mask select: VCC set by one SALU move per 8 selects, inside the same asm block
+__global__ __launch_bounds__(256) void k_cndmask_vcc(uint32_t *out, uint32_t c) {
+    STAMP(0)
+    uint32_t x[8];
+    for (int j = 0; j < 8; ++j) x[j] = threadIdx.x + j;
+    const uint64_t m = 0xAAAAAAAAAAAAAAAAull ^ c;
+    for (int i = 0; i < N_ITER; ++i) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            asm volatile("s_mov_b64 vcc, %8\n\t"
+                         "v_cndmask_b32 %0, %0, %9, vcc\n\tv_cndmask_b32 %1, %1, %9, vcc\n\t"
+                         "v_cndmask_b32 %2, %2, %9, vcc\n\tv_cndmask_b32 %3, %3, %9, vcc\n\t"
+                         "v_cndmask_b32 %4, %4, %9, vcc\n\tv_cndmask_b32 %5, %5, %9, vcc\n\t"
+                         "v_cndmask_b32 %6, %6, %9, vcc\n\tv_cndmask_b32 %7, %7, %9, vcc"
+                         : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+                         : "s"(m), "v"(c)
+                         : "vcc");
+        }
+    }
+    uint32_t r = 0;
+    for (int j = 0; j < 8; ++j) r ^= x[j];
+    out[blockIdx.x * 256 + threadIdx.x] = r;
+    STAMP(2)
+}
+
 // v_mad_u64_u32 writes a 64-bit result from two 32-bit sources
 __global__ __launch_bounds__(256) void k_mad_u64_u32(uint32_t *out, uint32_t c) {
     STAMP(0)
@@ -207,13 +283,16 @@ int main() {
         {"v_mul_lo_u32", k_mul_lo_u32}, {"v_mul_hi_u32", k_mul_hi_u32}, {"v_mad_u64_u32", k_mad_u64_u32},
         {"v_lshrrev_b64", k_lshr_b64}, {"v_lshl_add_u64", k_lshl_add_u64}, {"v_add_f64", k_add_f64},
         {"v_fma_f64", k_fma_f64}, {"v_add_f32", k_add_f32}, {"v_mul_f32", k_mul_f32}, {"v_max_f32", k_max_f32},
-        {"v_min3_f32", k_min3_f32}, {"v_cndmask_b32", k_cndmask}, {"v_mov_b32", k_mov_b32}, {"v_cmp_lt_f32", k_cmp_f32},
+        {"v_min3_f32", k_min3_f32}, {"v_cndmask_b32", k_cndmask_vcc}, {"v_mov_b32", k_mov_b32}, {"v_cmp_lt_f32", k_cmp_f32},
         {"v_sqrt_f32", k_sqrt_f32}, {"v_rcp_f32", k_rcp_f32}, {"v_cvt_f32_ubyte1", k_cvt_ubyte},
         {"v_pk_fma_f32", k_pk_fma_f32}, {"v_pk_add_f32", k_pk_add_f32}, {"v_pk_mul_f32", k_pk_mul_f32},
         {"v_mov_b64", k_mov_b64}, {"v_fmac_f32", k_fmac_f32}, {"v_sub_f32", k_sub_f32}, {"v_min_f32", k_min_f32},
         {"v_max_i32", k_max_i32}, {"v_med3_f32", k_med3_f32}, {"v_and_b32", k_and_b32}, {"v_lshlrev_b32", k_lshl_b32},
         {"v_bfe_u32", k_bfe_u32}, {"v_cndmask_b32 (sgpr mask)", k_cndmask_s}, {"v_perm_b32", k_perm_b32},
-        {"v_max_f32_e64", k_max_f32_e64}, {"v_mul_f32_e64", k_mul_f32_e64}, {"v_add3_u32", k_add3_u32}};
+        {"v_max_f32_e64", k_max_f32_e64}, {"v_mul_f32_e64", k_mul_f32_e64}, {"v_add3_u32", k_add3_u32},
+        {"v_fma_f32 (distinct)", k_fma_f32_d}, {"v_min3_f32 (distinct)", k_min3_f32_d},
+        {"v_med3_f32 (distinct)", k_med3_f32_d}, {"v_add3_u32 (distinct)", k_add3_u32_d},
+        {"v_cndmask_b32 (sgpr mask, distinct)", k_cndmask_s_d}, {"v_mad_u32_u24 (distinct)", k_mad_u32_u24_d}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
