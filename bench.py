@@ -30,10 +30,12 @@ Prints ONE JSON line (rank 0) with
     achieved = the wave-level VALU instructions of one launch (SQ_INSTS_VALU per
     sample from the committed rocprofv3 pass, profiles/r<NN>/traffic.json, for this
     very library build) over the kernel's live HIP-event time; peak = the rate 1,024
-    SIMDs x 2.4 GHz (peak engine clock) sustain on THIS kernel's instruction mix: each PMC instruction
-    class charged its microbenchmarked issue cost (tools/valu_issue_model.py:
-    ~2.4 cycles for f32 add/mul, integer add, logic and moves, ~4.2 for FMA,
-    min/max, compares, selects, shifts and 64-bit ops, ~8.2 for transcendentals).
+    SIMDs x 2.4 GHz (peak engine clock) sustain on THIS kernel's instructions, at the
+    issue cycles per instruction the same build's PMC pass measured: 4 x (SQ_ACTIVE_INST_VALU
+    - SQ_ACTIVE_INST_VALU2) / SQ_INSTS_VALU (one quad-cycle per wave64 instruction, two per
+    transcendental, two instructions in one quad-cycle when they dual-issue:
+    tools/lanes_summary.py).  frac_class_model keeps round 4's per-class model
+    (tools/valu_issue_model.py) for comparison.
     frac_uniform_2cyc keeps round 1's optimistic roof (every instruction 2 cycles).
     hbm_frac = PMC-measured HBM bytes per launch over the same time vs 8 TB/s;
     cache_served_bytes = SURVEY §8d's byte model.
@@ -68,7 +70,13 @@ CLOCK_GHZ = 2.4                # max engine clock (spec)
 VALU_CYCLES = 2                # a wave64 VALU instruction issues over 2 cycles on SIMD-32
 VALU_PEAK = SIMDS * CLOCK_GHZ * 1e9 / VALU_CYCLES   # wave-level VALU instructions / s
 METRIC = "Msamples/s (pixels×spp/s) + achieved HBM GB/s, final() 500×500×1000spp"   # BASELINE.json
-LAYOUT = "interleaved"         # rtnw.pixels_for_rank: rank (ry, rx) of a x b renders x = rx mod a, y = ry mod b
+# rtnw.pixels_for_rank (interleaved: rank (ry, rx) of a x b renders x = rx mod a, y = ry mod b)
+# or rtnw.blocks_for_rank (blocks: 8 x 8 pixel blocks dealt along a Hilbert curve)
+LAYOUT = os.environ.get("RTNW_LAYOUT", "interleaved")
+
+
+def rank_pixels(nx, ny, rank, world):
+    return (rtnw.blocks_for_rank if LAYOUT == "blocks" else rtnw.pixels_for_rank)(nx, ny, rank, world)
 
 
 def log(*a):
@@ -226,10 +234,12 @@ def read_profile(workload_key, sha=None):
 
 
 def read_lanes(workload_key, sha):
-    """VALU lane utilisation (SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)) of this
-    workload from the committed rocprofv3 pass of these very kernels
-    (profiles/r<NN>/lanes.json, tools/lanes_summary.py, matched by kernel_sha16), or
-    None when no pass of this build is committed."""
+    """VALU lane utilisation (SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU)) and the
+    measured issue cycles per VALU instruction (4 (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2)
+    / SQ_INSTS_VALU, None in passes without the dual-issue counter) of this workload from the
+    committed rocprofv3 pass of these very kernels (profiles/r<NN>/lanes.json,
+    tools/lanes_summary.py, matched by kernel_sha16), or None when no pass of this build is
+    committed."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9]*", "**", "lanes.json"), recursive=True),
                        reverse=True):
         try:
@@ -239,7 +249,8 @@ def read_lanes(workload_key, sha):
             continue
         c = t.get("configs", {}).get(workload_key)
         if sha and t.get("kernel_sha16") == sha and c and c.get("lane_utilisation"):
-            return c["lane_utilisation"], os.path.relpath(path, ROOT)
+            return c["lane_utilisation"], os.path.relpath(path, ROOT), c.get("issue_cycles_per_instr"), \
+                c.get("dual_issue_share")
     return None
 
 
@@ -368,9 +379,9 @@ def main():
     cam_name, bg, depth = rtnw.SCENE_DEFAULTS[scene_name]
     nx, ny = (w1, h1) if scaling == "strong" else image_for(world, w1, h1)
     if world > 1:
-        all_tiles = [rtnw.pixels_for_rank(nx, ny, r, world) for r in range(world)]
+        all_tiles = [rank_pixels(nx, ny, r, world) for r in range(world)]
     elif share:   # a rank's share alone (profiling; its image is that share's pixels)
-        all_tiles = [rtnw.pixels_for_rank(nx, ny, 0, share)]
+        all_tiles = [rank_pixels(nx, ny, 0, share)]
     else:
         all_tiles = [[(0, 0, nx, ny)]]
     all_counts = [int(np.asarray(t).reshape(-1, 4)[:, 2:].prod(axis=1).sum()) * 3 for t in all_tiles]
@@ -481,12 +492,12 @@ def main():
                 "segments_per_wave_iteration": cst["segments"] / max(1.0, cst["wave_iterations"])},
             "note": "the scene is L2/L1-resident: HBM carries ~1% of peak, the kernel is VALU-issue bound "
                     "(DESIGN.md §5c).  achieved = SQ_INSTS_VALU per sample (committed rocprofv3 pass of this "
-                    "library build) x samples / live kernel time; peak = 1024 SIMDs x 2.4 GHz / the mean "
-                    "issue cycles per instruction of this kernel's mix (PMC instruction classes x "
-                    "microbenchmarked costs, tools/valu_issue_model.py); frac_uniform_2cyc = the same "
-                    "instructions against 2 cycles each; traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 "
-                    "+ WRITE_SIZE); cache_served = SURVEY §8d byte model (node/primitive fetches, mostly "
-                    "L1/L2 hits)"}
+                    "library build) x samples / live kernel time; peak = 1024 SIMDs x 2.4 GHz / the issue "
+                    "cycles per instruction the same pass measured, 4 (SQ_ACTIVE_INST_VALU - "
+                    "SQ_ACTIVE_INST_VALU2) / SQ_INSTS_VALU (quad-cycles with dual issue; tools/lanes_summary.py); "
+                    "frac_class_model = round 4's per-class model; frac_uniform_2cyc = the same instructions "
+                    "against 2 cycles each; traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE); "
+                    "cache_served = SURVEY §8d byte model (node/primitive fetches, mostly L1/L2 hits)"}
     if prof:
         roof["profile"] = prof["path"]
         roof["profile_matches_library"] = sha in (prof.get("kernel_sha16"), prof.get("lib_sha16"))
@@ -509,7 +520,18 @@ def main():
         # computes for a lane (the headroom is idle lanes, not issue)
         lanes = read_lanes(f"c5_n{nshare}" if cfg == "c5" and nshare > 1 else cfg, sha)
         if lanes:
-            roof["lane_utilisation"], roof["lane_profile"] = lanes
+            roof["lane_utilisation"], roof["lane_profile"] = lanes[0], lanes[1]
+            if lanes[2] and roof["achieved"] is not None:
+                # the measured issue model (round 5): the VALU's own quad-cycle counters
+                # with dual issue, no instruction classes (tools/lanes_summary.py); the
+                # round-4 class model stays beside it as frac_class_model
+                roof["frac_class_model"] = roof["frac"]
+                roof["valu_issue_cycles_per_instr_class_model"] = roof["valu_issue_cycles_per_instr"]
+                roof["valu_issue_cycles_per_instr"] = lanes[2]
+                roof["dual_issue_share"] = lanes[3]
+                peak = SIMDS * CLOCK_GHZ * 1e9 / lanes[2]
+                roof["peak"] = peak / 1e9
+                roof["frac"] = roof["achieved"] * 1e9 / peak
             if roof["frac"] is not None:
                 roof["useful_frac"] = roof["frac"] * lanes[0]
             if roof["frac_uniform_2cyc"] is not None:

@@ -68,13 +68,6 @@ namespace {
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
-// Tail packing: once the pool is dry, a wave holding at most this many paths hands them
-// to another wave of its workgroup through LDS and retires (0: off)
-#ifndef RT_PACK_LANES
-#define RT_PACK_LANES 16
-#endif
-static_assert(RT_PACK_LANES <= 16, "a wave's packed paths fill its LDS rows at a stride of 16");
-
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -134,10 +127,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // per wave: the next RT_PRE work items' sample starts, made 64 at a time (refill)
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
-    // tail packing: the workgroup's mailbox, (waves still running << 16) | the waves whose
-    // paths wait in their LDS rows, and each such wave's path count
-    __shared__ uint32_t lds_mail;
-    __shared__ uint32_t lds_pack_n[kBlock / 64];
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
@@ -153,7 +142,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     if (threadIdx.x == 0) {
         store_camera(A, lds_cam);
         lds_mconst = LogConsts{1.0 / 7, -1.0 / 6, 0.2, -0.25, 1.0 / 3};
-        lds_mail = (uint32_t)(kBlock / 64) << 16;
     }
     for (uint32_t i = threadIdx.x; i < RT_LCG_JUMPS; i += kBlock) lds_jump[i] = kLcgJump.e[i];
     rtl_lds_init(threadIdx.x);   // rt_libm.h's sine constants
@@ -390,102 +378,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         phase = PH_IDLE;
     };
 
-    // ---- tail packing (RT_PACK_LANES) ---------------------------------------------
-    // Once the pool is dry, a wave holding at most RT_PACK_LANES paths writes them into its
-    // own LDS rows (its cooperative slots and sample-start slots, which nothing reads once
-    // it retires), publishes them in the workgroup's mailbox and retires; a dry wave with
-    // free lanes takes them in.  The launch's last paths then run in a few full waves
-    // instead of many nearly empty ones sharing each SIMD's issue.  A path moves with its
-    // item, sample range, depth, item sum, ray, throughput and drand48 states and restarts
-    // its segment's closest-hit search from the root (the hit does not depend on where the
-    // search started: the (t, key) order), so the image is bitwise unchanged.  The mailbox
-    // changes only by compare-and-swap: a wave retires — donating, or empty-handed — only
-    // while another wave still runs, and empty-handed only when no paths wait, so no path
-    // is ever stranded; every retirement removes a wave, so the exchange terminates.
-    constexpr bool kPack = RT_PACK_LANES > 0;
-    constexpr uint32_t kPackWords = kMedia ? 21u : 19u;
-    auto pack_row = [&](uint32_t w, uint32_t k) -> uint32_t * {   // dword k of wave w's paths, 16 paths a row
-        return k < 16u ? reinterpret_cast<uint32_t *>(lds_slots[w]) + k * 16u
-                       : reinterpret_cast<uint32_t *>(lds_pre_key[w]) + (k - 16u) * 16u;
-    };
-    auto pack_put = [&](uint32_t i) {   // this lane's path into its wave's rows, as path i
-        const uint32_t v[21] = {item, (uint32_t)s_cur, (uint32_t)s_end, (uint32_t)depth,
-                                __float_as_uint(part.x), __float_as_uint(part.y), __float_as_uint(part.z),
-                                __float_as_uint(r.o.x), __float_as_uint(r.o.y), __float_as_uint(r.o.z),
-                                __float_as_uint(r.d.x), __float_as_uint(r.d.y), __float_as_uint(r.d.z),
-                                __float_as_uint(r.time), __float_as_uint(beta.x), __float_as_uint(beta.y),
-                                __float_as_uint(beta.z), (uint32_t)g.x, (uint32_t)(g.x >> 32),
-                                (uint32_t)g.xm, (uint32_t)(g.xm >> 32)};
-#pragma unroll
-        for (uint32_t k = 0; k < kPackWords; ++k) pack_row(wave, k)[i] = v[k];
-    };
-    auto pack_get = [&](uint32_t d, uint32_t i) {   // path i of wave d into this lane
-        uint32_t v[21];
-#pragma unroll
-        for (uint32_t k = 0; k < kPackWords; ++k) v[k] = pack_row(d, k)[i];
-        item = v[0]; s_cur = (int)v[1]; s_end = (int)v[2]; depth = (int)v[3];
-        part = mk(__uint_as_float(v[4]), __uint_as_float(v[5]), __uint_as_float(v[6]));
-        r.o = mk(__uint_as_float(v[7]), __uint_as_float(v[8]), __uint_as_float(v[9]));
-        r.d = mk(__uint_as_float(v[10]), __uint_as_float(v[11]), __uint_as_float(v[12]));
-        r.time = __uint_as_float(v[13]);
-        beta = mk(__uint_as_float(v[14]), __uint_as_float(v[15]), __uint_as_float(v[16]));
-        g.x = ((uint64_t)v[18] << 32) | v[17];
-        if (kMedia) g.xm = ((uint64_t)v[20] << 32) | v[19];
-        finished = false;
-        pre_have = false;
-        begin_segment();
-        if (kCount) cnt.segments--;   // the donor counted this segment
-    };
-    typedef __attribute__((address_space(3))) uint32_t LdsU32;
-    auto mail_read = [&]() -> uint32_t {
-        return __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load((LdsU32 *)&lds_mail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-    };
-    auto mail_cas = [&](uint32_t expect, uint32_t want) -> bool {   // one lane's compare-and-swap, the wave's verdict
-        int ok = 0;
-        if (first_active()) {
-            uint32_t e = expect;
-            ok = __hip_atomic_compare_exchange_strong((LdsU32 *)&lds_mail, &e, want, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
-        }
-        return __builtin_amdgcn_readfirstlane(ok) != 0;
-    };
-    // A dry wave's exchange at the top of an iteration; true: the wave retires.
-    auto pack_exchange = [&](uint64_t &live) -> bool {
-        for (;;) {
-            const uint32_t w = mail_read();
-            const uint32_t alive = w >> 16, mask = w & 0xFFFFu;
-            const uint32_t nlive = (uint32_t)__popcll(live);
-            if (mask != 0u) {   // take the first waiting wave's paths if they fit the free lanes
-                const uint32_t d = (uint32_t)__builtin_ctz(mask);
-                const uint32_t n = __builtin_amdgcn_readfirstlane(
-                    __hip_atomic_load((LdsU32 *)&lds_pack_n[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (n <= 64u - nlive) {
-                    if (!mail_cas(w, w & ~(1u << d))) continue;
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                    const bool fr = finished;
-                    const uint32_t rk = lanes_below(wballot(fr));
-                    if (fr && rk < n) pack_get(d, rk);
-                    live = wballot(!finished);
-                    continue;
-                }
-            }
-            if (nlive == 0u) {   // nothing to run and (n <= 16 always fits) nothing waiting
-                if (mail_cas(w, w - (1u << 16))) return true;
-                continue;
-            }
-            if (nlive <= (uint32_t)RT_PACK_LANES && alive > 1u && wballot(!finished && phase != PH_TRAV) == 0ull) {
-                if (!finished) pack_put(lanes_below(live));
-                if (first_active())
-                    __hip_atomic_store((LdsU32 *)&lds_pack_n[wave], nlive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (mail_cas(w, (w - (1u << 16)) | (1u << wave))) return true;
-                continue;
-            }
-            return false;
-        }
-    };
-
     for (;;) {
         // (not in the flat-scan variant: its scan reads the group records right at the
         // iteration's start, and the reload measured slower there, c2 37.63 -> 37.88 ms)
@@ -495,10 +387,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // cooperative rounds: a metal's absorbed reflection; the others start their
         // next sample inside stage 5)
         retire_and_claim();
-        uint64_t live = wballot(!finished);
-        if (kPack && exhausted && pre_count == 0) {
-            if (pack_exchange(live)) break;
-        }
+        const uint64_t live = wballot(!finished);
         if (live == 0ull) break;
         // the pool is dry and few paths are left: the launch's end waits on their latency
         const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
@@ -918,5 +807,5 @@ extern "C" int rt_megakernel_lds_static_actual(void) {
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 + 16 +
-                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8) + RT_LCG_JUMPS * 16 + 4 + (RT_LDS_BLOCK / 64) * 4) + 256;
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8) + RT_LCG_JUMPS * 16) + 256;
 }

@@ -486,6 +486,56 @@ def pixels_for_rank(nx, ny, rank, world, block=8):
     return t
 
 
+def hilbert_index(n, x, y):
+    """Position of cell (x, y) on the Hilbert curve over an n x n grid (n a power of 2)."""
+    x = np.asarray(x, dtype=np.int64).copy()
+    y = np.asarray(y, dtype=np.int64).copy()
+    d = np.zeros_like(x)
+    s = n // 2
+    while s > 0:
+        rx = (x & s) > 0
+        ry = (y & s) > 0
+        d += s * s * ((3 * rx) ^ ry)
+        # rotate the quadrant
+        flip = ~ry
+        sw = flip & rx
+        x = np.where(sw, s - 1 - x, x)
+        y = np.where(sw, s - 1 - y, y)
+        x, y = np.where(flip, y, x), np.where(flip, x, y)
+        s //= 2
+    return d
+
+
+def blocks_for_rank(nx, ny, rank, world, block=8):
+    """Block deal: the image's block x block pixel blocks, in Hilbert-curve order, dealt to
+    the ranks in turn (block k to rank k mod world) — every rank's blocks spread evenly
+    over the view (equal counts +-1), and each block keeps the 1-GPU render's ray
+    coherence: a wave's 64 items are one 8 x 8 block (pixels_for_rank's lattice spreads
+    them over a x 8 by b x 8 pixels).  Returned as 1x1 tiles, block by block, each block
+    column by column."""
+    bx, by = (nx + block - 1) // block, (ny + block - 1) // block
+    n = 1
+    while n < max(bx, by):
+        n *= 2
+    X, Y = np.meshgrid(np.arange(bx), np.arange(by), indexing="xy")
+    d = hilbert_index(n, X.ravel(), Y.ravel())
+    order = np.argsort(d, kind="stable")
+    mine = order[rank::world]
+    out = []
+    for k in mine:
+        x0, y0 = int(X.ravel()[k]) * block, int(Y.ravel()[k]) * block
+        xs = np.arange(x0, min(x0 + block, nx))
+        ys = np.arange(y0, min(y0 + block, ny))
+        I, J = np.meshgrid(xs, ys, indexing="ij")   # column by column
+        out.append(np.stack([I.ravel(), J.ravel()], axis=1))
+    if not out:
+        return np.zeros((0, 4), np.int32)
+    xy = np.concatenate(out)
+    t = np.ones((xy.shape[0], 4), np.int32)
+    t[:, :2] = xy
+    return t
+
+
 def rank_layout(nx, ny, tile, world, order="diagonal"):
     """Tiles and packed float counts of every rank."""
     if order == "interleaved":

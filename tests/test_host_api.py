@@ -281,3 +281,28 @@ def test_shared_reciprocal_division_is_ieee(tmp_path):
     out = subprocess.run([exe, "20000000"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.strip().startswith("0 mismatches")
+
+
+def test_block_deal_partitions_the_image():
+    """rtnw.blocks_for_rank (the 8 x 8 block deal along a Hilbert curve, bench.py
+    RTNW_LAYOUT=blocks and tools/scaling_probe.py --layout blocks): the ranks' pixels
+    partition the image, counts within one block, each block's 64 pixels consecutive."""
+    for nx, ny, world in [(1000, 1000, 8), (37, 23, 3), (64, 8, 2)]:
+        seen = np.zeros((ny, nx), int)
+        counts = []
+        for r in range(world):
+            t = rtnw.blocks_for_rank(nx, ny, r, world)
+            counts.append(len(t))
+            seen[t[:, 1], t[:, 0]] += 1
+            if nx % 8 == 0 and ny % 8 == 0 and len(t):
+                blk = t[:, :2].reshape(-1, 64, 2) // 8
+                assert (blk == blk[:, :1]).all()
+        assert (seen == 1).all()
+        assert max(counts) - min(counts) <= 64
+    # consecutive Hilbert indices are neighbouring cells
+    n = 16
+    X, Y = np.meshgrid(np.arange(n), np.arange(n), indexing="xy")
+    d = rtnw.hilbert_index(n, X.ravel(), Y.ravel())
+    o = np.argsort(d)
+    assert np.array_equal(np.sort(d), np.arange(n * n))
+    assert (np.abs(np.diff(X.ravel()[o])) + np.abs(np.diff(Y.ravel()[o])) == 1).all()

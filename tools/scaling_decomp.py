@@ -60,7 +60,9 @@ def main():
     res["c5"] = {"points_ms_samples": c5, "fixed_ms": f1, "steady_ns_per_sample": k1 * 1e6}
     print(f"c5 1 GPU: fixed {f1:.3f} ms, steady {k1 * 1e6:.4f} ns/sample, 1000 spp {t1:.2f} ms", flush=True)
     for n in args.shares:
-        pts = [kernel_ms(["--share-of", str(n), "--spp", str(spp)], args.lib) for spp in (1000, 2000, 4000)]
+        # three spp from 1000 up to what one launch holds (the 16 GiB slab: 12 B per sample)
+        top = min(4000, (16 << 30) // (12 * (1000 * 1000 // n)) // 500 * 500)
+        pts = [kernel_ms(["--share-of", str(n), "--spp", str(spp)], args.lib) for spp in (1000, (1000 + top) // 2, top)]
         f, k = fit(pts)
         t, s = pts[0]
         base = t1 / s1   # the 1-GPU image's measured cost per sample

@@ -37,9 +37,9 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="default: the config's (c5: 1000)")
     ap.add_argument("--repeats", type=int, default=3, help="median of this many launches per share")
     ap.add_argument("--out", default="")
-    ap.add_argument("--layout", default="interleaved", choices=["interleaved", "diagonal", "hashed"],
-                    help="interleaved: rtnw.pixels_for_rank (bench.py's); diagonal / hashed: --tile blocks "
-                         "(rtnw.tiles_for_rank)")
+    ap.add_argument("--layout", default="interleaved", choices=["interleaved", "blocks", "diagonal", "hashed"],
+                    help="interleaved: rtnw.pixels_for_rank; blocks: rtnw.blocks_for_rank (8 x 8 blocks dealt along "
+                         "a Hilbert curve); diagonal / hashed: --tile blocks (rtnw.tiles_for_rank)")
     ap.add_argument("--tile", type=int, default=8)
     args = ap.parse_args()
 
@@ -53,13 +53,15 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     out = torch.zeros(nx * ny * 3, dtype=torch.float32, device=dev)
     res = {"config": args.config, "image": [nx, ny], "spp": spp, "layout": args.layout,
-           "tile": args.tile if args.layout != "interleaved" else 1, "runs": []}
+           "tile": args.tile if args.layout != "interleaved" else 1, "kernel_sha16": bench.kernel_sha16(), "runs": []}
     base = None
     for n in [int(x) for x in args.ranks.split(",")]:
         if n == 1:
             shares = [[(0, 0, nx, ny)]]
         elif args.layout == "interleaved":
             shares = [rtnw.pixels_for_rank(nx, ny, r, n) for r in range(n)]
+        elif args.layout == "blocks":
+            shares = [rtnw.blocks_for_rank(nx, ny, r, n, args.tile) for r in range(n)]
         else:
             shares = [rtnw.tiles_for_rank(nx, ny, args.tile, r, n, args.layout) for r in range(n)]
         scene.render_tiles(cam, params, shares[0], out.data_ptr(), stream)   # warm
