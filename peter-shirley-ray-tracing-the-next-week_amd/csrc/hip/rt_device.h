@@ -736,6 +736,26 @@ struct LdsNodes {   // node references are byte offsets (n * 16) into the planes
     __device__ __forceinline__ const float4 *ptr8q(uint32_t) const { return nullptr; }
 };
 
+// The traversal stack: one column per lane, [depth][lane] (a wave's push or pop is one
+// conflict-free ds_write_b32 / ds_read_b32), addressed by the depth `sp` with one shift-add.
+// RT_SP_BYTES = 1 (A/B): sp holds the byte offset (depth x 256) instead, so the address is
+// one fast add — but the conditional +-256 steps become selects (4-cycle VALU) where the
+// depth steps were carry-in adds, and c4's variant spilled 8 B.
+#ifndef RT_SP_BYTES
+#define RT_SP_BYTES 0
+#endif
+#if RT_SP_BYTES
+#define RT_SP_UNIT 256
+__device__ __forceinline__ uint32_t &stk_at(uint32_t *stk, int sp) {
+    return *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(stk) + sp);
+}
+#else
+#define RT_SP_UNIT 1
+__device__ __forceinline__ uint32_t &stk_at(uint32_t *stk, int sp) {   // one shift-add per address
+    return *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(stk) + ((uint32_t)sp << 8));
+}
+#endif
+
 // 8-wide node step's tail: the nearest hit child (the first one in slot order on
 // ties) is the next node, the other hit children are pushed in reverse slot order.
 // The builder puts the children in slots by direction from the node's centre (slot
@@ -754,8 +774,8 @@ __device__ __forceinline__ uint32_t wide8_tail(const float k[8], const uint32_t 
     }
 #pragma unroll
     for (int c = 7; c >= 0; --c) {   // slot written, then kept only if pushed
-        stk[sp * 64] = ch[c];
-        sp += (k[c] != RT_INF && c != sel) ? 1 : 0;
+        stk_at(stk, sp) = ch[c];
+        sp += (k[c] != RT_INF && c != sel) ? RT_SP_UNIT : 0;
     }
     return next;
 }
@@ -779,8 +799,8 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
         const bool lt = tn1 < tn0;
         const bool second = h1 & (!h0 | lt);
         const uint32_t nearc = second ? c1 : (h0 ? c0 : RT_EMPTY_CHILD), farc = second ? c0 : c1;
-        stk[sp * 64] = farc;
-        const int sp0 = h0 ? sp + 1 : sp;
+        stk_at(stk, sp) = farc;
+        const int sp0 = h0 ? sp + RT_SP_UNIT : sp;
         sp = h1 ? sp0 : sp;
         return nearc;
     } else if (kWidth == 2) {   // rt_dnode2
@@ -797,8 +817,8 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
         const bool lt = tn1 < tn0;
         const bool second = h1 & (!h0 | lt);           // ties: child 0 first (no short circuit: no branch)
         const uint32_t nearc = second ? c1 : (h0 ? c0 : RT_EMPTY_CHILD), farc = second ? c0 : c1;
-        stk[sp * 64] = farc;                           // kept only if both children were hit
-        const int sp0 = h0 ? sp + 1 : sp;
+        stk_at(stk, sp) = farc;                        // kept only if both children were hit
+        const int sp0 = h0 ? sp + RT_SP_UNIT : sp;
         sp = h1 ? sp0 : sp;
         return nearc;
     } else if (kWidth == 8) {   // rt_dnode8
@@ -859,12 +879,12 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
         cas(k0, c0, k2, c2);
         cas(k1, c1, k3, c3);
         cas(k1, c1, k2, c2);
-        stk[sp * 64] = c3;
-        sp += k3 != RT_INF;
-        stk[sp * 64] = c2;
-        sp += k2 != RT_INF;
-        stk[sp * 64] = c1;
-        sp += k1 != RT_INF;
+        stk_at(stk, sp) = c3;
+        sp += k3 != RT_INF ? RT_SP_UNIT : 0;
+        stk_at(stk, sp) = c2;
+        sp += k2 != RT_INF ? RT_SP_UNIT : 0;
+        stk_at(stk, sp) = c1;
+        sp += k1 != RT_INF ? RT_SP_UNIT : 0;
         return k0 != RT_INF ? c0 : RT_EMPTY_CHILD;
     }
 }
@@ -917,8 +937,8 @@ __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, 
             pleaf = park ? node : pleaf;
             node = park ? RT_EMPTY_CHILD : node;
             const bool pop = node == RT_EMPTY_CHILD && sp > 0;
-            sp -= pop ? 1 : 0;
-            const uint32_t top = stk[(uint32_t)sp * 64u];   // sp >= 0: pops only from a non-empty stack
+            sp -= pop ? RT_SP_UNIT : 0;
+            const uint32_t top = stk_at(stk, sp);   // sp >= 0: pops only from a non-empty stack
             node = pop ? top : node;
         }
         if (__popcll(wballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD)) <= kTail) {
@@ -1288,6 +1308,11 @@ __device__ __forceinline__ void scan_group(const ConstF4 *P, int q, int kinds, i
 // volatile read at each use, so the compiler neither hoists them into registers held
 // across the persistent loop (where they were spilled to scratch) nor folds them back.
 typedef LogConsts MediaConsts;   // log_f64's coefficients
+// how the media stage reads them: 0 the round-4 way (only 0.2 from LDS; with the glibc sine
+// inlined it spilled -1/6), 1 five volatile reads, 2 one record copy read at the use
+#ifndef RT_LOG_CONSTS
+#define RT_LOG_CONSTS 2
+#endif
 typedef __attribute__((address_space(3))) const volatile MediaConsts LdsMediaConsts;
 // constant_medium::hit for every medium after the surface search
 // (constant_medium.h:26-50): the boundary's entry/exit, clipped to [t_min, best]
@@ -1363,7 +1388,18 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     r1 = r1 < 0 ? 0.f : r1;
     const float distance_inside_boundary = (r2 - r1) * dlen;
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
-    const float hit_distance = (float)((double)neg_inv_density * log_f64(u48x(xk), LogConsts{mc->c07, mc->c06, mc->c02, mc->c025, mc->c03}));
+#if RT_LOG_CONSTS == 0   // round 4's: 0.2 from LDS, the rest immediates
+    const LogConsts lc{1.0 / 7, -1.0 / 6, mc->c02, -0.25, 1.0 / 3};
+#elif RT_LOG_CONSTS == 1  // each coefficient by its own volatile LDS read
+    const LogConsts lc{mc->c07, mc->c06, mc->c02, mc->c025, mc->c03};
+#elif !defined(__HIP_DEVICE_COMPILE__)   // (the host pass never runs device code)
+    const LogConsts lc{mc->c07, mc->c06, mc->c02, mc->c025, mc->c03};
+#else                     // one copy of the record through an opaque LDS address: read at the use, vectorised
+    uint32_t mca = (uint32_t)(size_t)mc;
+    asm volatile("" : "+v"(mca));
+    const LogConsts lc = *(__attribute__((address_space(3))) const LogConsts *)(size_t)mca;
+#endif
+    const float hit_distance = (float)((double)neg_inv_density * log_f64(u48x(xk), lc));
     const bool hit = ok && hit_distance < distance_inside_boundary;
     const float tm = r1 + div_by(hit_distance, rd);
     best_t = hit ? tm : best_t;
