@@ -306,3 +306,17 @@ def test_block_deal_partitions_the_image():
     o = np.argsort(d)
     assert np.array_equal(np.sort(d), np.arange(n * n))
     assert (np.abs(np.diff(X.ravel()[o])) + np.abs(np.diff(Y.ravel()[o])) == 1).all()
+
+
+def test_math_probe_rejects_bad_arguments():
+    """rt_math_probe (the device-transcendental diagnostic) validates before touching the GPU."""
+    RT_ERR_INVALID = -1   # include/rt_hip.h
+    L = rtnw.lib()
+    x = np.zeros(4, np.float32)
+    out = np.zeros(4, np.float32)
+    assert L.rt_math_probe(6, x.ctypes.data, x.ctypes.data, out.ctypes.data, 4) == RT_ERR_INVALID
+    assert L.rt_math_probe(-1, x.ctypes.data, x.ctypes.data, out.ctypes.data, 4) == RT_ERR_INVALID
+    assert b"rt_math_probe" in L.rt_last_error()
+    assert L.rt_math_probe(4, x.ctypes.data, None, out.ctypes.data, 4) == RT_ERR_INVALID   # atan2f needs b
+    assert L.rt_math_probe(0, None, None, out.ctypes.data, 4) == RT_ERR_INVALID
+    assert L.rt_math_probe(0, None, None, None, 0) == rtnw.RT_OK   # nothing to do
