@@ -1309,7 +1309,9 @@ __device__ __forceinline__ void scan_group(const ConstF4 *P, int q, int kinds, i
 // across the persistent loop (where they were spilled to scratch) nor folds them back.
 typedef LogConsts MediaConsts;   // log_f64's coefficients
 // how the media stage reads them: 0 the round-4 way (only 0.2 from LDS; with the glibc sine
-// inlined it spilled -1/6), 1 five volatile reads, 2 one record copy read at the use
+// inlined it spills, c4 +1.4 %), 1 five volatile reads, 2 one record copy read at the use
+// (1 and 2 measure alike: profiles/r05/ab_log_consts_ocml_r04.log; 0.2 and -1/6 alone
+// from LDS spill too)
 #ifndef RT_LOG_CONSTS
 #define RT_LOG_CONSTS 2
 #endif
