@@ -5,7 +5,7 @@ PROFILE_DIR (profiles/rNN/), the layout bench.py's roofline reads:
 
   PROFILE_DIR/{traffic.json,pmc_summary.md,valu_issue_model.json}   c4 (tools/pmc_traffic.py)
   PROFILE_DIR/<cfg>/...                                             c5, c5_nN, c3, c2
-  PROFILE_DIR/pmc/<cfg>/pmc_{fetch,write,l2,sq,lanes}.csv, classes/pmc_classes_{1,2}.csv
+  PROFILE_DIR/pmc/<cfg>/pmc_{fetch,write,l2,sq,lds,lanes}.csv, classes/pmc_classes_{1,2}.csv
   PROFILE_DIR/lanes.json                                            tools/lanes_summary.py
   PROFILE_DIR/valu_rates.log                                        the issue-cost microbenchmark
   PROFILE_DIR/final/{bench_*.log,prof.log}, kernel_stats_c4.csv     tools/final_bench.sh
@@ -52,7 +52,7 @@ def main():
         subprocess.run([sys.executable, os.path.join(HERE, "pmc_traffic.py"), src, dst, str(samples_of(cfg)), cfg],
                        check=True, env=env, stdout=subprocess.DEVNULL)
         pd = os.path.join(prof, "pmc", cfg)
-        for k in ("fetch", "write", "l2", "sq"):
+        for k in ("fetch", "write", "l2", "sq", "lds"):
             cp(os.path.join(src, f"pmc_{k}", "run_counter_collection.csv"), os.path.join(pd, f"pmc_{k}.csv"))
         for i in (1, 2):
             cp(os.path.join(src, "classes", f"pass{i}", "run_counter_collection.csv"),
