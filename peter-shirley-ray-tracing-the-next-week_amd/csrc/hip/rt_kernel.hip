@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(lds_dyn + 4 * RT_LDS_NODE_CAP) +
+    uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_dyn) + RT_LDS_NODE_BYTES_K) +
                                wave * (uint32_t)A.stack_depth * 64u + lane
                          : &lds_stack[kMode ? 0 : wave][0][lane];
     CoopSlot *slots = lds_slots[wave];
@@ -154,9 +154,22 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const float4 b0 = N[0], b1 = N[1], b2 = N[2];
             float4 cf = N[3];
             const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
+#if RT_LDS_SPLIT
+            cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : rt_split_addr(c0));
+            cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : rt_split_addr(c1));
+            // one dword per node and value (rt_device.h RtSplit), value k at k * RT_SPLIT_PB
+            char *P = reinterpret_cast<char *>(lds_dyn) + rt_split_addr(i);
+            auto put = [&](int k, float v) { *reinterpret_cast<float *>(P + k * RT_SPLIT_PB) = v; };
+            put(RS_C0, cf.x); put(RS_C1, cf.y);
+            put(RS_XLO, b0.x); put(RS_XLO + 1, b1.z); put(RS_XHI, b0.y); put(RS_XHI + 1, b1.w);
+            put(RS_YLO, b0.z); put(RS_YLO + 1, b2.x); put(RS_YHI, b0.w); put(RS_YHI + 1, b2.y);
+            put(RS_ZLO, b1.x); put(RS_ZLO + 1, b2.z); put(RS_ZHI, b1.y); put(RS_ZHI + 1, b2.w);
+#else
             cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : c0 << 4);
             cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : c1 << 4);
-#if RT_LDS_SIGNED
+#endif
+#if RT_LDS_SPLIT
+#elif RT_LDS_SIGNED
             // the references, then per-axis planes (LdsNodes::load_signed): (lo0, hi0, lo1, hi1) of x, y, z
             lds_dyn[i] = cf;
             lds_dyn[i + RT_LDS_NODE_CAP] = make_float4(b0.x, b0.y, b1.z, b1.w);
@@ -228,7 +241,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     bool fresh = false;   // a new segment the pre-scan has not seen yet
     auto begin_segment = [&]() {
         if (kPrescan) fresh = true;
-        node = kLds ? A.root << 4 : A.root;   // LDS mode: byte offsets (the root is interior there)
+        // LDS mode: byte offsets (the root is interior there)
+        node = kLds ? (RT_LDS_SPLIT ? rt_split_addr(A.root) : A.root << 4) : A.root;
         sp = 0;
         best_t = RT_FLT_MAX;
         best_key = 0x7FFFFFFF;
@@ -713,7 +727,7 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
     auto *k = rt_megakernel<kCount, kProf, kWidth, kFeat, kLds>;
     size_t dyn = 0;
     if (kLds == 1) {
-        dyn = RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES(a->stack_depth);
+        dyn = RT_LDS_NODE_BYTES_K + RT_LDS_STACK_BYTES(a->stack_depth);
         // Dynamic LDS above the default limit: the attribute (the most any scene can
         // ask for) is set once per device and variant, recorded in an atomic bit mask
         // (thread-safe; calling hipFuncSetAttribute before every launch cost ~0.6 ms
