@@ -629,54 +629,44 @@ __device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, fl
 #ifndef RT_LDS_SIGNED
 #define RT_LDS_SIGNED 1
 #endif
-// RT_LDS_SPLIT (with RT_LDS_SIGNED): every value of a node in a plane of its own, one dword
+// kSplit = 1 (RT_LDS_SIGNED layouts): every value of a node in a plane of its own, one dword
 // per node — 14 planes of RT_LDS_NODE_CAP dwords: the child references c0, c1, then x-lo,
-// x-hi, y-lo, y-hi, z-lo, z-hi of child 0 and child 1 in turn (RtSplit::*) — so the values
-// of both children for one axis and side are one plane (4 KiB) apart and load as one
-// ds_read2st64_b32, and lanes at different nodes hit 64 banks by node index instead of the
-// 16 a float4-per-node plane leaves them (c4's PMC pass: 26 % of the LDS-active cycles
-// were bank-conflict cycles, profiles/r05/pmc/c4/pmc_lds.csv).  56 KiB instead of 64.
-// RT_LDS_SPLIT = 2: the same 14 values per node, in blocks of 32 nodes: block b holds, for
-// each value k, the 32 nodes' dwords in a row of 128 B ([block][value][node]).  The two
-// children's values of one axis and side are then 32 dwords apart (one ds_read2_b32,
-// offset1:32, in two different banks — in the plane layout above both fall in one bank), and
-// lanes at different nodes spread by node index mod 32.
-// RT_LDS_SPLIT = 3: the 14 values of a node consecutive, nodes 15 dwords apart (an odd
-// stride): value k of node n in bank (15 n + k) mod 32, so lanes at different nodes spread
-// over all 32 banks, and a pair (child 0, child 1) is two adjacent banks (ds_read2_b32
-// offset1:1).  (Planes or 32-node blocks put both children of a pair in ONE bank: the LDS
-// has 32 banks — their conflict cycles rose 0.26 → 0.33 of the LDS-active cycles.)
-#ifndef RT_LDS_SPLIT
-#define RT_LDS_SPLIT 0
-#endif
+// x-hi, y-lo, y-hi, z-lo, z-hi of child 0 and child 1 in turn (RtSplit) — so the values of
+// both children for one axis and side are one plane (4 KiB) apart and load as one
+// ds_read2st64_b32; 56 KiB instead of 64.  The media variants (final()) use it: final() c4
+// 51.52 -> 51.33 ms, its c5 rank share of 8 26.77 -> 26.63, c5 199.5 -> 198.6, while the
+// random scenes' variant measured slower with it (c3 44.06 -> 44.28) and keeps the float4
+// planes (profiles/r05/ab_lds_split_layouts.log).  The gain is not fewer bank conflicts —
+// it has more: the LDS has 32 banks and both values of a pair fall in one (0.26 -> 0.33 of
+// the LDS-active cycles); blocks of 32 nodes conflict the same, an odd 15-dword node stride
+// conflicts least (0.20) and was slower on final() (+0.45 %): profiles/r05/lds_layouts/.
 enum RtSplit { RS_C0 = 0, RS_C1 = 1, RS_XLO = 2, RS_XHI = 4, RS_YLO = 6, RS_YHI = 8, RS_ZLO = 10, RS_ZHI = 12, RS_PLANES = 14 };
-// byte distance between value k and value k + 1 of one node
-#define RT_SPLIT_PB (RT_LDS_SPLIT == 3 ? 4 : RT_LDS_SPLIT == 2 ? 128 : RT_LDS_NODE_CAP * 4)
-// byte offset of node n's first value
-__host__ __device__ __forceinline__ uint32_t rt_split_addr(uint32_t n) {
-    return RT_LDS_SPLIT == 3 ? n * 60 : RT_LDS_SPLIT == 2 ? (n >> 5) * (RS_PLANES * 128) + (n & 31) * 4 : n * 4;
-}
-// node bytes of the LDS layout the kernel uses (the host sizes the LDS by the larger one)
-#define RT_LDS_NODE_BYTES_K                                                                          \
-    (RT_LDS_SPLIT == 3 ? 15 * RT_LDS_NODE_CAP * 4 : RT_LDS_SPLIT ? RS_PLANES * RT_LDS_NODE_CAP * 4 : RT_LDS_NODE_BYTES)
+#define RT_SPLIT_PB (RT_LDS_NODE_CAP * 4)   // bytes per dword plane
+// node bytes of the LDS layout (the host sizes the LDS by the larger, float4 one)
+template <int kSplit>
+constexpr uint32_t lds_node_bytes() { return kSplit ? RS_PLANES * RT_SPLIT_PB : RT_LDS_NODE_BYTES; }
+// an interior node's reference: its byte offset in a plane
+template <int kSplit>
+__host__ __device__ __forceinline__ uint32_t lds_node_ref(uint32_t n) { return kSplit ? n * 4 : n * 16; }
 struct Slab { F2 ix, iy, iz, nox, noy, noz; float tmin; uint32_t lx, ly, lz, fx, fy, fz; };
+template <int kSplit = 0>
 __device__ __forceinline__ Slab make_slab(const Ray &r, float tmin) {
     const float ix = __builtin_amdgcn_rcpf(r.d.x), iy = __builtin_amdgcn_rcpf(r.d.y), iz = __builtin_amdgcn_rcpf(r.d.z);
     Slab s;
     s.ix = F2{ix, ix}; s.iy = F2{iy, iy}; s.iz = F2{iz, iz};
     s.nox = F2{-r.o.x * ix, -r.o.x * ix}; s.noy = F2{-r.o.y * iy, -r.o.y * iy}; s.noz = F2{-r.o.z * iz, -r.o.z * iz};
     s.tmin = tmin;
-#if RT_LDS_SPLIT
-    const uint32_t sx = __float_as_uint(ix) >> 31, sy = __float_as_uint(iy) >> 31, sz = __float_as_uint(iz) >> 31;
-    s.lx = (RS_XLO + 2 * sx) * RT_SPLIT_PB; s.fx = (RS_XHI - 2 * sx) * RT_SPLIT_PB;
-    s.ly = (RS_YLO + 2 * sy) * RT_SPLIT_PB; s.fy = (RS_YHI - 2 * sy) * RT_SPLIT_PB;
-    s.lz = (RS_ZLO + 2 * sz) * RT_SPLIT_PB; s.fz = (RS_ZHI - 2 * sz) * RT_SPLIT_PB;
-#else
-    s.lx = ((__float_as_uint(ix) >> 31) << 2) + RT_LDS_NODE_CAP * 16;
-    s.ly = ((__float_as_uint(iy) >> 31) << 2) + 2 * RT_LDS_NODE_CAP * 16;
-    s.lz = ((__float_as_uint(iz) >> 31) << 2) + 3 * RT_LDS_NODE_CAP * 16;
-    s.fx = s.lx ^ 4u; s.fy = s.ly ^ 4u; s.fz = s.lz ^ 4u;
-#endif
+    if (kSplit) {
+        const uint32_t sx = __float_as_uint(ix) >> 31, sy = __float_as_uint(iy) >> 31, sz = __float_as_uint(iz) >> 31;
+        s.lx = (RS_XLO + 2 * sx) * RT_SPLIT_PB; s.fx = (RS_XHI - 2 * sx) * RT_SPLIT_PB;
+        s.ly = (RS_YLO + 2 * sy) * RT_SPLIT_PB; s.fy = (RS_YHI - 2 * sy) * RT_SPLIT_PB;
+        s.lz = (RS_ZLO + 2 * sz) * RT_SPLIT_PB; s.fz = (RS_ZHI - 2 * sz) * RT_SPLIT_PB;
+    } else {
+        s.lx = ((__float_as_uint(ix) >> 31) << 2) + RT_LDS_NODE_CAP * 16;
+        s.ly = ((__float_as_uint(iy) >> 31) << 2) + 2 * RT_LDS_NODE_CAP * 16;
+        s.lz = ((__float_as_uint(iz) >> 31) << 2) + 3 * RT_LDS_NODE_CAP * 16;
+        s.fx = s.lx ^ 4u; s.fy = s.ly ^ 4u; s.fz = s.lz ^ 4u;
+    }
     return s;
 }
 // entry distance of one child box, +inf if the ray misses it (or, kSlots, the slot
@@ -735,7 +725,8 @@ struct GlobalNodes {
 // other word: near/far come out of the load, not out of a min and a max per axis
 // and child (12 VALU per node step for 6 address adds).  Without RT_LDS_SIGNED the
 // planes are the node's 4 float4 (rt_layout.h).
-struct LdsNodes {   // node references are byte offsets (n * 16) into the planes
+template <int kSplit = 0>
+struct LdsNodes {   // node references are byte offsets (n * 16, kSplit: n * 4) into the planes
     const LdsF4 *p;
     __device__ __forceinline__ void load2(uint32_t n, float4 &b0, float4 &b1, float4 &b2, float4 &cf) const {
         const LdsF4 *N = (const LdsF4 *)((__attribute__((address_space(3))) const char *)p + n);
@@ -755,32 +746,31 @@ struct LdsNodes {   // node references are byte offsets (n * 16) into the planes
                                                 uint32_t &c0, uint32_t &c1) const {
         typedef __attribute__((address_space(3))) const float LdsF;
         typedef __attribute__((address_space(3))) const char LdsC;
-#if RT_LDS_SPLIT
-        // (child 0, child 1): one value apart — one ds_read2st64_b32 (planes) / ds_read2_b32 (blocks)
-        auto pair = [&](uint32_t a) {
-            const LdsF *q = (const LdsF *)(size_t)(n + a);
-            return F2{q[0], q[RT_SPLIT_PB / 4]};
-        };
-        nx = pair(s.lx); fx = pair(s.fx);
-        ny = pair(s.ly); fy = pair(s.fy);
-        nz = pair(s.lz); fz = pair(s.fz);
-        typedef __attribute__((address_space(3))) const uint32_t LdsU;
-        const LdsU *C = (const LdsU *)((LdsC *)p + n);
-        c0 = C[0]; c1 = C[RT_SPLIT_PB / 4];
-#else
-        auto pair = [&](uint32_t a) {   // (child 0, child 1) at one address: one ds_read2_b32
-            const LdsF *q = (const LdsF *)(size_t)(n + a);
-            return F2{q[0], q[2]};
-        };
-        nx = pair(s.lx); fx = pair(s.fx);
-        ny = pair(s.ly); fy = pair(s.fy);
-        nz = pair(s.lz); fz = pair(s.fz);
-        typedef unsigned U2v __attribute__((ext_vector_type(2)));
-        const __attribute__((address_space(3))) U2v *C =
-            (const __attribute__((address_space(3))) U2v *)((LdsC *)p + n);
-        const U2v c = *C;
-        c0 = c.x; c1 = c.y;
-#endif
+        if constexpr (kSplit) {
+            auto pair = [&](uint32_t a) {   // (child 0, child 1): one plane apart, one ds_read2st64_b32
+                const LdsF *q = (const LdsF *)(size_t)(n + a);
+                return F2{q[0], q[RT_LDS_NODE_CAP]};
+            };
+            nx = pair(s.lx); fx = pair(s.fx);
+            ny = pair(s.ly); fy = pair(s.fy);
+            nz = pair(s.lz); fz = pair(s.fz);
+            typedef __attribute__((address_space(3))) const uint32_t LdsU;
+            const LdsU *C = (const LdsU *)((LdsC *)p + n);
+            c0 = C[0]; c1 = C[RT_LDS_NODE_CAP];
+        } else {
+            auto pair = [&](uint32_t a) {   // (child 0, child 1) at one address: one ds_read2_b32
+                const LdsF *q = (const LdsF *)(size_t)(n + a);
+                return F2{q[0], q[2]};
+            };
+            nx = pair(s.lx); fx = pair(s.fx);
+            ny = pair(s.ly); fy = pair(s.fy);
+            nz = pair(s.lz); fz = pair(s.fz);
+            typedef unsigned U2v __attribute__((ext_vector_type(2)));
+            const __attribute__((address_space(3))) U2v *C =
+                (const __attribute__((address_space(3))) U2v *)((LdsC *)p + n);
+            const U2v c = *C;
+            c0 = c.x; c1 = c.y;
+        }
     }
     __device__ __forceinline__ const float4 *ptr4(uint32_t) const { return nullptr; }   // wide BVHs stay in HBM
     __device__ __forceinline__ const float4 *ptr8(uint32_t) const { return nullptr; }
@@ -837,7 +827,7 @@ __device__ __forceinline__ uint32_t wide8_tail(const float k[8], const uint32_t 
 template <int kWidth, class Nodes>
 __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, const Slab &s, float best_t, uint32_t *stk,
                                               int &sp) {
-    if constexpr (kWidth == 2 && RT_LDS_SIGNED && std::is_same<Nodes, LdsNodes>::value) {
+    if constexpr (kWidth == 2 && RT_LDS_SIGNED && !std::is_same<Nodes, GlobalNodes>::value) {
         F2 nx, ny, nz, fx, fy, fz;
         uint32_t c0, c1;
         src.load_signed(node, s, nx, ny, nz, fx, fy, fz, c0, c1);

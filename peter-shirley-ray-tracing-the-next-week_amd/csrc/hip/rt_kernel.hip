@@ -65,6 +65,11 @@ namespace {
 #endif
 
 
+// The LDS node layout of the media variants (rt_device.h RtSplit): 1 dword planes, 0 float4 planes
+#ifndef RT_LDS_SPLIT_MEDIA
+#define RT_LDS_SPLIT_MEDIA 1
+#endif
+
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
@@ -117,6 +122,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0,
                    kMedia = (kFeat & RT_FEAT_MEDIA) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
+    // the LDS node layout (rt_device.h RtSplit): dword planes in the media variants (final()),
+    // float4 planes otherwise, as each measured fastest
+    constexpr int kSplit = (kLds && kMedia && RT_LDS_SIGNED && kWidth == 2) ? RT_LDS_SPLIT_MEDIA : 0;
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
     __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : (kWidth >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH)][64];
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
@@ -131,7 +139,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_dyn) + RT_LDS_NODE_BYTES_K) +
+    uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_dyn) + lds_node_bytes<kSplit>()) +
                                wave * (uint32_t)A.stack_depth * 64u + lane
                          : &lds_stack[kMode ? 0 : wave][0][lane];
     CoopSlot *slots = lds_slots[wave];
@@ -154,22 +162,18 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const float4 b0 = N[0], b1 = N[1], b2 = N[2];
             float4 cf = N[3];
             const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-#if RT_LDS_SPLIT
-            cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : rt_split_addr(c0));
-            cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : rt_split_addr(c1));
-            // one dword per node and value (rt_device.h RtSplit), value k at k * RT_SPLIT_PB
-            char *P = reinterpret_cast<char *>(lds_dyn) + rt_split_addr(i);
-            auto put = [&](int k, float v) { *reinterpret_cast<float *>(P + k * RT_SPLIT_PB) = v; };
-            put(RS_C0, cf.x); put(RS_C1, cf.y);
-            put(RS_XLO, b0.x); put(RS_XLO + 1, b1.z); put(RS_XHI, b0.y); put(RS_XHI + 1, b1.w);
-            put(RS_YLO, b0.z); put(RS_YLO + 1, b2.x); put(RS_YHI, b0.w); put(RS_YHI + 1, b2.y);
-            put(RS_ZLO, b1.x); put(RS_ZLO + 1, b2.z); put(RS_ZHI, b1.y); put(RS_ZHI + 1, b2.w);
-#else
-            cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : c0 << 4);
-            cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : c1 << 4);
-#endif
-#if RT_LDS_SPLIT
-#elif RT_LDS_SIGNED
+            cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : lds_node_ref<kSplit>(c0));
+            cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : lds_node_ref<kSplit>(c1));
+            if constexpr (kSplit) {   // one dword per node and plane (rt_device.h RtSplit)
+                float *P = reinterpret_cast<float *>(lds_dyn) + i;
+                constexpr uint32_t C = RT_LDS_NODE_CAP;
+                P[RS_C0 * C] = cf.x; P[RS_C1 * C] = cf.y;
+                P[RS_XLO * C] = b0.x; P[(RS_XLO + 1) * C] = b1.z; P[RS_XHI * C] = b0.y; P[(RS_XHI + 1) * C] = b1.w;
+                P[RS_YLO * C] = b0.z; P[(RS_YLO + 1) * C] = b2.x; P[RS_YHI * C] = b0.w; P[(RS_YHI + 1) * C] = b2.y;
+                P[RS_ZLO * C] = b1.x; P[(RS_ZLO + 1) * C] = b2.z; P[RS_ZHI * C] = b1.y; P[(RS_ZHI + 1) * C] = b2.w;
+                continue;
+            }
+#if RT_LDS_SIGNED
             // the references, then per-axis planes (LdsNodes::load_signed): (lo0, hi0, lo1, hi1) of x, y, z
             lds_dyn[i] = cf;
             lds_dyn[i + RT_LDS_NODE_CAP] = make_float4(b0.x, b0.y, b1.z, b1.w);
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     }
     __syncthreads();
     const GlobalNodes gnodes{A.nodes};
-    const LdsNodes lnodes{(const LdsF4 *)lds_dyn};
+    const LdsNodes<kSplit> lnodes{(const LdsF4 *)lds_dyn};
 
     const uint64_t skey = seed_key(A.seed);   // per-launch part of the sample keys
     // wave-uniform claim pool, and the pre-made sample starts [pre_head, pre_head + pre_count)
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     auto begin_segment = [&]() {
         if (kPrescan) fresh = true;
         // LDS mode: byte offsets (the root is interior there)
-        node = kLds ? (RT_LDS_SPLIT ? rt_split_addr(A.root) : A.root << 4) : A.root;
+        node = kLds ? lds_node_ref<kSplit>(A.root) : A.root;
         sp = 0;
         best_t = RT_FLT_MAX;
         best_key = 0x7FFFFFFF;
@@ -432,7 +436,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 // operands, no LDS round trip per primitive (an LDS copy: c2 52.58 -> 51.93 ms)
                 const ConstF4 *P = (const ConstF4 *)A.prims;
                 const ConstF4 *G = (const ConstF4 *)A.groups;
-                const Slab sl = make_slab(r, A.tmin);
+                const Slab sl = make_slab<kSplit>(r, A.tmin);
                 ScanBest b{best_t, 0x7FFFFFFF};   // a new segment: nothing found yet
                 for (int gi = 0; gi < A.ngroups; ++gi) {
                     const F4v gh = G[3 * gi], bx = G[3 * gi + 1], bz = G[3 * gi + 2];
@@ -469,7 +473,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 if (__popcll(wballot(phase == PH_READY)) >= RT_READY_BATCH) break;
                 if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
-                    Slab sl = make_slab(r, A.tmin);
+                    Slab sl = make_slab<kSplit>(r, A.tmin);
                     uint32_t pleaf;
                     if constexpr (kLds && RT_LDS_SIGNED && kWidth == 2) lnodes.prepare(sl);
                     if constexpr (kLds)
@@ -727,7 +731,7 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
     auto *k = rt_megakernel<kCount, kProf, kWidth, kFeat, kLds>;
     size_t dyn = 0;
     if (kLds == 1) {
-        dyn = RT_LDS_NODE_BYTES_K + RT_LDS_STACK_BYTES(a->stack_depth);
+        dyn = RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES(a->stack_depth);   // (the dword planes need less)
         // Dynamic LDS above the default limit: the attribute (the most any scene can
         // ask for) is set once per device and variant, recorded in an atomic bit mask
         // (thread-safe; calling hipFuncSetAttribute before every launch cost ~0.6 ms

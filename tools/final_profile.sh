@@ -26,6 +26,9 @@ for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:l2" 
   echo "== pmc $name"
   timeout -s KILL 240 rocprofv3 --pmc $ctrs -d $O/pmc_$name -o run --output-format csv -- $B > $O/pmc_$name.log 2>&1
 done
+echo "== pmc lds"   # LDS bank / address conflicts and waits
+timeout -s KILL 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_UNALIGNED_STALL SQ_WAVE_CYCLES \
+    -d $O/pmc_lds -o run --output-format csv -- $B > $O/pmc_lds.log 2>&1
 echo "== pmc lanes"   # VALU lane utilisation (tools/lanes_summary.py reads gpurun_out/lanes_<cfg>)
 timeout -s KILL 240 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU -d gpurun_out/lanes_$CFG -o run \
     --output-format csv -- $B > $O/pmc_lanes.log 2>&1
