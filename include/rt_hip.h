@@ -23,9 +23,8 @@
 extern "C" {
 #endif
 
-/* 2: rt_stats gained the shading-stage divergence fields (wave_shade_passes ...)
- * 3: rt_stats gained the medium cell's fields (cell_prims, cell_segments) */
-#define RT_ABI_VERSION 3
+/* 2: rt_stats gained the shading-stage divergence fields (wave_shade_passes ...) */
+#define RT_ABI_VERSION 2
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -221,8 +220,6 @@ typedef struct rt_stats {
     double lane_scatters;         /*   lanes that scattered (SIMD efficiency = this / 64x wave_shade_passes) */
     double cycles_scatter;        /* RT_FLAG_PROFILE: wave cycles in the material scatter branches (part of
                                          cycles_shade) */
-    double cell_prims;            /* BVH scenes with media: primitives near the medium cell's ball, 0 without a cell */
-    double cell_segments;         /* RT_FLAG_COUNT: segments whose closest hit the medium cell decided (no descent) */
 } rt_stats;
 
 typedef struct rt_scene rt_scene; /* opaque; owns device copies */

@@ -510,7 +510,7 @@ __device__ __forceinline__ bool first_active() { return lanes_below(wballot(1)) 
 
 struct Counters {
     uint64_t samples = 0, segments = 0, nodes = 0, spheres = 0, mspheres = 0, rects = 0, instanced = 0, media = 0,
-             shades = 0, noise = 0, cell = 0;
+             shades = 0, noise = 0;
     // wave-level trip counts (SIMD efficiency = lane-level count / (64 x wave-level count))
     uint64_t w_iters = 0, w_nodes = 0, w_prims = 0, w_rius = 0, l_rius = 0;
     // material divergence of the shading stage: wave passes through the scatter

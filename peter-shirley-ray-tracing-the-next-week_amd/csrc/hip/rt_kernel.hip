@@ -70,11 +70,6 @@ namespace {
 #define RT_LDS_SPLIT_MEDIA 1
 #endif
 
-// The medium cell's shortcut of the closest-hit search (stage 3; capi.cpp rt_scene_create)
-#ifndef RT_CELL
-#define RT_CELL 1
-#endif
-
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
@@ -127,7 +122,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0,
                    kMedia = (kFeat & RT_FEAT_MEDIA) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
-    constexpr bool kCell = kMedia && !kScan && RT_CELL;   // the medium cell (stage 3; capi.cpp)
     // the LDS node layout (rt_device.h RtSplit): dword planes in the media variants (final()),
     // float4 planes otherwise, as each measured fastest
     constexpr int kSplit = (kLds && kMedia && RT_LDS_SIGNED && kWidth == 2) ? RT_LDS_SPLIT_MEDIA : 0;
@@ -250,7 +244,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // a new ray segment: closest-hit search from the root (hitable_list.h:20-32)
     bool fresh = false;   // a new segment the pre-scan has not seen yet
     auto begin_segment = [&]() {
-        if (kPrescan || kCell) fresh = true;
+        if (kPrescan) fresh = true;
         // LDS mode: byte offsets (the root is interior there)
         node = kLds ? lds_node_ref<kSplit>(A.root) : A.root;
         sp = 0;
@@ -464,33 +458,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 if (act) phase = PH_READY;
             }
         } else {
-            // the medium cell (capi.cpp): a new segment starting inside the ball tests the
-            // primitives near it; a hit before the ray leaves the ball is the closest of
-            // all (every other primitive lies outside), and the search ends without a descent
-            if (kCell && A.cell_n > 0) {
-                bool in = false;
-                float tsafe = 0.f;
-                if (fresh && phase == PH_TRAV) {
-                    const V3 oc = sub(r.o, mk(A.cell_c[0], A.cell_c[1], A.cell_c[2]));
-                    const float a = dot(r.d, r.d), b = dot(oc, r.d), cc = dot(oc, oc) - A.cell_r2;
-                    if (cc < 0.f && a > 0.f) {
-                        // where the ray leaves the ball: the larger root, without cancellation
-                        // (approximate square root and reciprocals, ~1 ulp each: a bound, not a result)
-                        const float q = __builtin_amdgcn_sqrtf(b * b - a * cc);
-                        const float te = b >= 0.f ? -cc * __builtin_amdgcn_rcpf(b + q) : (q - b) * __builtin_amdgcn_rcpf(a);
-                        tsafe = te * (1.f - 1.f / 4096);   // below it by far more than its rounding
-                        in = true;
-                    }
-                }
-                if (wballot(in) != 0ull) {
-                    lockstep_prims<kCount, kInst, true>((const ConstF4 *)A.prims, A.cell_first, A.cell_n, A.insts, r, A.tmin,
-                                                        in, -1, best_t, best_key, best_prim, cnt);
-                    if (in && best_t < tsafe) {
-                        phase = PH_READY;
-                        if (kCount) cnt.cell++;
-                    }
-                }
-            }
             // pre-scan: the scene's largest primitives (capi.cpp), kept out of the BVH,
             // tested in lockstep by every lane with a new segment before its descent;
             // their hits also shorten best_t, which culls more of the BVH
@@ -499,8 +466,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 if (wballot(fr) != 0ull)
                     lockstep_prims<kCount, kInst, true>((const ConstF4 *)A.prims, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
                                                         best_t, best_key, best_prim, cnt);
+                fresh = false;
             }
-            if (kPrescan || kCell) fresh = false;
             for (;;) {
                 if (wballot(phase == PH_TRAV) == 0ull) break;
                 if (__popcll(wballot(phase == PH_READY)) >= RT_READY_BATCH) break;
@@ -684,7 +651,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
 
     if (kCount) {
         uint64_t v[RT_CNT_N] = {cnt.samples, cnt.segments, cnt.nodes, cnt.spheres, cnt.mspheres, cnt.rects,
-                                cnt.instanced, cnt.media, cnt.shades, cnt.noise, cnt.cell};
+                                cnt.instanced, cnt.media, cnt.shades, cnt.noise};
         for (int k = 0; k < RT_CNT_N; ++k) {
             uint64_t x = v[k];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off);

@@ -157,10 +157,6 @@ struct rt_scene {
          *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr, *groups = nullptr;
     bool scan = false;            // flat scan of the primitive groups instead of the BVH (small scenes)
     int nprescan = 0;             // BVH scenes: largest primitives tested in lockstep before the BVH
-    // medium cell (rt_scene_create): primitives [cell_first, cell_first + cell_n) are copies of those near the ball
-    int cell_first = 0, cell_n = 0;
-    float cell_c[3] = {0, 0, 0}, cell_r2 = 0;
-    std::vector<int> cell_prims;
     int ngroups = 0;
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
@@ -452,53 +448,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
                          ((g.kinds >> 24) & 0xff) + g.nyz;
         if (runs != g.count) return cleanup(fail(RT_ERR_INVALID, "flat scan: a group's kind counts do not add up"));
     }
-    // Medium cell (BVH modes; rt_kernel.hip stage 3): a path inside a dense medium scatters
-    // there segment after segment, and every segment's closest-hit search starts from the
-    // BVH root.  For one medium bounded by a sphere (c, R) — the densest such — the
-    // primitives whose boxes reach within R + m of c (m = R / 64 + 1e-3 |c|) are listed
-    // (at most RT_CELL_MAX, appended to the device primitives as copies: same record, same
-    // key); a ray starting within R + m / 2 of c tests just them first, and if the nearest
-    // lies before the ray leaves that ball, no other primitive (all are outside R + m) can
-    // be nearer: the search ends there, with the same (t, key) winner as the full one.
-    // RTNW_CELL=0 disables it (A/B).
-    s->cell_n = 0;
-    if (!s->scan && d->nprims > 0) {
-        bool want = true;
-        if (const char *e = std::getenv("RTNW_CELL")) want = std::atoi(e) != 0;
-        double best_density = -1;
-        for (int i = 0; want && i < d->nmedia; i++) {
-            const rt_medium &m = d->media[i];
-            if (m.boundary_count != 1) continue;
-            const rt_prim &bp = d->boundary_prims[m.boundary_first];
-            if (bp.kind != RT_PRIM_SPHERE || bp.instance >= 0 || !(m.density > best_density)) continue;
-            const double c[3] = {bp.p[0], bp.p[1], bp.p[2]}, R = std::fabs((double)bp.p[3]);
-            const double cmax = std::max(std::fabs(c[0]), std::max(std::fabs(c[1]), std::fabs(c[2])));
-            const double mg = R / 64 + 1e-3 * cmax, reach = R + mg;
-            if (!(R > 0) || !std::isfinite(reach)) continue;
-            std::vector<int> near;
-            for (int q = 0; q < d->nprims && (int)near.size() <= RT_CELL_MAX; q++) {
-                float lo[3], hi[3];
-                rtnw::prim_bounds(d->prims[q], d->instances, d->time0, d->time1, lo, hi);
-                double d2 = 0;
-                for (int k = 0; k < 3; k++) {
-                    const double v = std::max(std::max((double)lo[k] - c[k], c[k] - (double)hi[k]), 0.0);
-                    d2 += v * v;
-                }
-                if (!(d2 > reach * reach)) near.push_back(q);   // (a NaN box counts as near)
-            }
-            if (near.empty() || (int)near.size() > RT_CELL_MAX) continue;
-            best_density = m.density;
-            s->cell_n = (int)near.size();
-            s->cell_first = (int)order.size();
-            for (int k = 0; k < 3; k++) s->cell_c[k] = (float)c[k];
-            const double rk = R + mg / 2;
-            s->cell_r2 = (float)(rk * rk);
-            s->cell_prims = near;
-        }
-        for (int q : s->cell_prims) order.push_back(q);
-    }
-    std::vector<rt_dprim> prims(order.size()), bprims(d->nboundary);
-    for (int i = 0; i < (int)order.size(); i++) {
+    std::vector<rt_dprim> prims(d->nprims), bprims(d->nboundary);
+    for (int i = 0; i < d->nprims; i++) {
         const int src = order[i];
         prims[i] = to_dprim(d->prims[src], src);
         s->has_moving |= d->prims[src].kind == RT_PRIM_MOVING_SPHERE;
@@ -789,10 +740,6 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.groups = (const float4 *)s->groups;
     a.ngroups = s->ngroups;
     a.nprescan = s->nprescan;
-    a.cell_first = s->cell_first;
-    a.cell_n = s->cell_n;
-    for (int k = 0; k < 3; k++) a.cell_c[k] = s->cell_c[k];
-    a.cell_r2 = s->cell_r2;
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
@@ -923,7 +870,6 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->medium_tests = (double)c[RT_CNT_MEDIA];
             stats->shades = (double)c[RT_CNT_SHADES];
             stats->noise_evals = (double)c[RT_CNT_NOISE];
-            stats->cell_segments = (double)c[RT_CNT_CELL];
             stats->algorithmic_bytes = algorithmic_bytes(*stats, (double)s->npix * (double)nchunks_total, s->bvh_width);
             unsigned long long w[5];
             HIP_TRY(hipMemcpy(w, (unsigned long long *)s->stats + RT_STAT_WAVE, sizeof w, hipMemcpyDeviceToHost));
@@ -959,7 +905,6 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         stats->lds_level = s->lds_nodes ? 1.0 : 0.0;
         stats->scan_groups = s->scan ? (double)s->ngroups : 0.0;
         stats->prescan = (double)s->nprescan;
-        stats->cell_prims = (double)s->cell_n;
         stats->stack_depth = (double)(s->lds_nodes ? s->stack_depth : s->bvh_width >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH);
     }
     return RT_OK;

@@ -107,7 +107,6 @@ struct rt_dprim {
 #define RT_SCAN_MAX 64
 // BVH scenes: at most this many of the largest primitives are pre-scanned (capi.cpp).
 #define RT_PRESCAN_MAX 8
-#define RT_CELL_MAX 16   // primitives near a medium cell's ball (capi.cpp), tested in lockstep
 struct rt_dgroup {
     int32_t first, count, instance, kinds;
     float bx[4], bz[2];
@@ -149,7 +148,7 @@ struct rt_dmedium {
 // Counters of the RT_FLAG_COUNT kernel variant (uint64 each).
 enum {
     RT_CNT_SAMPLES = 0, RT_CNT_SEGMENTS, RT_CNT_NODES, RT_CNT_SPHERES, RT_CNT_MSPHERES, RT_CNT_RECTS,
-    RT_CNT_INSTANCED, RT_CNT_MEDIA, RT_CNT_SHADES, RT_CNT_NOISE, RT_CNT_CELL, RT_CNT_N
+    RT_CNT_INSTANCED, RT_CNT_MEDIA, RT_CNT_SHADES, RT_CNT_NOISE, RT_CNT_N
 };
 // The rest of the stats buffer (uint64 slots after the RT_CNT_N counters): stage
 // cycles (RT_FLAG_PROFILE), wave-level trip counts (RT_FLAG_COUNT), the wave

@@ -95,7 +95,7 @@ class RtStats(ctypes.Structure):
         "wave_node_trips", "wave_prim_trips", "wave_sphere_draw_trips", "lane_sphere_draw_trips", "chunk",
         "batches", "lds_level", "stack_depth", "scan_groups", "prescan", "wave_exhaust_first_us",
         "wave_exhaust_last_us", "wave_end_first_us", "wave_end_mean_us", "wave_end_last_us",
-        "wave_shade_passes", "wave_shade_kinds", "lane_scatters", "cycles_scatter", "cell_prims", "cell_segments")]
+        "wave_shade_passes", "wave_shade_kinds", "lane_scatters", "cycles_scatter")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
