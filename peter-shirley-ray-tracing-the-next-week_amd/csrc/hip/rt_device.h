@@ -1514,13 +1514,16 @@ __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool re
     float nscale = (RT_SHADE_LEAN & 32) ? unset_f() : 0.f;     // read for the noisy lanes only
     if (shading) {
         if (kCount) cnt.shades++;
-        st.kind = fbits(A.mats[hr.mat * 2 + 0].x);
+        const float4 m0 = A.mats[hr.mat * 2 + 0], m1 = A.mats[hr.mat * 2 + 1];
+        st.kind = fbits(m0.x);
         st.live = depth < A.max_depth;
         const bool textured = st.kind == RT_MAT_DIFFUSE_LIGHT ||
                               (st.live && (st.kind == RT_MAT_LAMBERTIAN || st.kind == RT_MAT_ISOTROPIC));
-        if (textured) {
+        if (textured && (fbits(m1.w) & 2)) {   // a constant texture, resolved by the host (capi.cpp)
+            st.tv = mk(m1.x, m1.y, m1.z);
+        } else if (textured) {
             float4 t0, t1;
-            const int tkind = tex_leaf<kChecker>(A, fbits(A.mats[hr.mat * 2 + 0].y), hr.p, t0, t1);   // texture.h:35-44
+            const int tkind = tex_leaf<kChecker>(A, fbits(m0.y), hr.p, t0, t1);   // texture.h:35-44
             noisy = tkind == RT_TEX_NOISE;
             nscale = t0.w;
             if (!noisy) st.tv = tex_value_leaf<kUV>(A, tkind, t0, t1, hr.u, hr.v);

@@ -489,6 +489,15 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         }
         o.flags = (m.texture >= 0 && reads_uv(m.texture)) ? 1 : 0;
         s->has_uv |= o.flags != 0;
+        // a textured material (lambertian, isotropic, diffuse_light) whose texture is a
+        // constant: its color in the unused albedo slots, flag 2 (shade_begin then reads
+        // no texture record: one dependent load fewer per shade)
+        const bool textured = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_ISOTROPIC || m.kind == RT_MAT_DIFFUSE_LIGHT;
+        if (RT_MAT_CONST_TEX && textured && m.texture >= 0 && m.texture < d->ntextures &&
+            d->textures[m.texture].kind == RT_TEX_CONSTANT) {
+            for (int k = 0; k < 3; k++) o.albedo[k] = d->textures[m.texture].color[k];
+            o.flags |= 2;
+        }
         s->has_specular |= m.kind == RT_MAT_METAL || m.kind == RT_MAT_DIELECTRIC;
     }
     std::vector<rt_dtexture> texs(d->ntextures);
