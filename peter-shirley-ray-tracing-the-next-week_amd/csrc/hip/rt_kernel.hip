@@ -731,7 +731,9 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
     auto *k = rt_megakernel<kCount, kProf, kWidth, kFeat, kLds>;
     size_t dyn = 0;
     if (kLds == 1) {
-        dyn = RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES(a->stack_depth);   // (the dword planes need less)
+        // the variant's node layout (rt_megakernel's kSplit): dword planes need 56 KiB, float4 planes 64
+        constexpr int kSplitL = ((kFeat & RT_FEAT_MEDIA) != 0 && RT_LDS_SIGNED && kWidth == 2) ? RT_LDS_SPLIT_MEDIA : 0;
+        dyn = lds_node_bytes<kSplitL>() + RT_LDS_STACK_BYTES(a->stack_depth);
         // Dynamic LDS above the default limit: the attribute (the most any scene can
         // ask for) is set once per device and variant, recorded in an atomic bit mask
         // (thread-safe; calling hipFuncSetAttribute before every launch cost ~0.6 ms
@@ -742,8 +744,12 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
         if (e != hipSuccess) return e;
         const uint64_t bit = 1ull << (dev & 63);
         if (!(done.load(std::memory_order_acquire) & bit)) {
+            // the most the budget leaves beside this variant's own static arrays
+            hipFuncAttributes fa;
+            e = hipFuncGetAttributes(&fa, (const void *)k);
+            if (e != hipSuccess) return e;
             e = hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    RT_LDS_BUDGET - rt_megakernel_lds_static_bytes());
+                                    RT_LDS_BUDGET - (int)fa.sharedSizeBytes);
             if (e != hipSuccess) return e;
             done.fetch_or(bit, std::memory_order_release);
         }
