@@ -76,7 +76,8 @@ LAYOUT = os.environ.get("RTNW_LAYOUT", "interleaved")
 
 
 def rank_pixels(nx, ny, rank, world):
-    return (rtnw.blocks_for_rank if LAYOUT == "blocks" else rtnw.pixels_for_rank)(nx, ny, rank, world)
+    fn = {"blocks": rtnw.blocks_for_rank, "lattice": rtnw.lattice_blocks_for_rank}.get(LAYOUT, rtnw.pixels_for_rank)
+    return fn(nx, ny, rank, world)
 
 
 def log(*a):

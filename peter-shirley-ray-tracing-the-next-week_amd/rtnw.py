@@ -536,6 +536,31 @@ def blocks_for_rank(nx, ny, rank, world, block=8):
     return t
 
 
+def lattice_blocks_for_rank(nx, ny, rank, world, block=8):
+    """Block lattice: with world = a x b, rank (ry, rx) = divmod(rank, a) renders the
+    block x block pixel blocks (bx, by) with bx = rx (mod a), by = ry (mod b) — the pixel
+    interleave's regular sub-sampling of the view at block granularity, so each wave's
+    64 items stay one 8 x 8 block (the 1-GPU render's ray coherence).  Returned as 1x1
+    tiles, block by block in row-major block order, each block column by column."""
+    a, b = interleave_factors(world)
+    ry, rx = divmod(rank, a)
+    bx, by = (nx + block - 1) // block, (ny + block - 1) // block
+    out = []
+    for yb in range(ry, by, b):
+        for xb in range(rx, bx, a):
+            x0, y0 = xb * block, yb * block
+            xs = np.arange(x0, min(x0 + block, nx))
+            ys = np.arange(y0, min(y0 + block, ny))
+            I, J = np.meshgrid(xs, ys, indexing="ij")   # column by column
+            out.append(np.stack([I.ravel(), J.ravel()], axis=1))
+    if not out:
+        return np.zeros((0, 4), np.int32)
+    xy = np.concatenate(out)
+    t = np.ones((xy.shape[0], 4), np.int32)
+    t[:, :2] = xy
+    return t
+
+
 def rank_layout(nx, ny, tile, world, order="diagonal"):
     """Tiles and packed float counts of every rank."""
     if order == "interleaved":

@@ -283,6 +283,21 @@ def test_shared_reciprocal_division_is_ieee(tmp_path):
     assert out.stdout.strip().startswith("0 mismatches")
 
 
+def test_block_lattice_partitions_the_image():
+    """rtnw.lattice_blocks_for_rank (8 x 8 blocks on the a x b interleave lattice, bench.py
+    RTNW_LAYOUT=lattice): the ranks' pixels partition the image, each block's 64 pixels
+    consecutive and one block."""
+    for nx, ny, world in [(1000, 1000, 8), (37, 23, 3), (64, 8, 2), (500, 500, 4)]:
+        seen = np.zeros((ny, nx), int)
+        for r in range(world):
+            t = rtnw.lattice_blocks_for_rank(nx, ny, r, world)
+            seen[t[:, 1], t[:, 0]] += 1
+            if nx % 8 == 0 and ny % 8 == 0 and len(t):
+                blk = t[:, :2].reshape(-1, 64, 2) // 8
+                assert (blk == blk[:, :1]).all()
+        assert (seen == 1).all()
+
+
 def test_block_deal_partitions_the_image():
     """rtnw.blocks_for_rank (the 8 x 8 block deal along a Hilbert curve, bench.py
     RTNW_LAYOUT=blocks and tools/scaling_probe.py --layout blocks): the ranks' pixels

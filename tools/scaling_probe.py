@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--spp", type=int, default=0, help="default: the config's (c5: 1000)")
     ap.add_argument("--repeats", type=int, default=3, help="median of this many launches per share")
     ap.add_argument("--out", default="")
-    ap.add_argument("--layout", default="interleaved", choices=["interleaved", "blocks", "diagonal", "hashed"],
+    ap.add_argument("--layout", default="interleaved", choices=["interleaved", "blocks", "lattice", "diagonal", "hashed"],
                     help="interleaved: rtnw.pixels_for_rank; blocks: rtnw.blocks_for_rank (8 x 8 blocks dealt along "
                          "a Hilbert curve); diagonal / hashed: --tile blocks (rtnw.tiles_for_rank)")
     ap.add_argument("--tile", type=int, default=8)
@@ -62,6 +62,8 @@ def main():
             shares = [rtnw.pixels_for_rank(nx, ny, r, n) for r in range(n)]
         elif args.layout == "blocks":
             shares = [rtnw.blocks_for_rank(nx, ny, r, n, args.tile) for r in range(n)]
+        elif args.layout == "lattice":
+            shares = [rtnw.lattice_blocks_for_rank(nx, ny, r, n, args.tile) for r in range(n)]
         else:
             shares = [rtnw.tiles_for_rank(nx, ny, args.tile, r, n, args.layout) for r in range(n)]
         scene.render_tiles(cam, params, shares[0], out.data_ptr(), stream)   # warm
