@@ -12,9 +12,11 @@ Workloads (BASELINE.json configs):
       main.cpp:254-259, 500 x 500 x 1000 spp, depth 50, black background.
   N > 1 (default c5): final() 1000 x 1000 x 1000 spp split over the N ranks —
       strong scaling, total work fixed (the config BASELINE quotes for 8 GPUs).
-      The pixels are interleaved over the ranks (N = a x b, rank (ry, rx) renders
-      x = rx mod a, y = ry mod b: a sub-sampled copy of the whole view, so every
-      rank's expected cost is the same), then ONE gather to rank 0: by default the
+      The image's 8 x 8 pixel blocks are dealt to the ranks in turn along a Hilbert
+      curve (rtnw.blocks_for_rank: every rank's blocks spread evenly over the view,
+      and a wave's 64 items stay one coherent block; RTNW_LAYOUT=interleaved selects
+      the pixel interleave, =lattice the block lattice), then ONE
+      gather to rank 0: by default the
       C ABI's rt_dist_gather (ncclGather on its own RCCL communicator, rccl.h:745,
       over xGMI), or `--gather torch` (torch.distributed.gather).  `--dist-backend
       gloo` gathers through host memory so the multi-rank path can be rehearsed with
@@ -70,9 +72,20 @@ CLOCK_GHZ = 2.4                # max engine clock (spec)
 VALU_CYCLES = 2                # a wave64 VALU instruction issues over 2 cycles on SIMD-32
 VALU_PEAK = SIMDS * CLOCK_GHZ * 1e9 / VALU_CYCLES   # wave-level VALU instructions / s
 METRIC = "Msamples/s (pixels×spp/s) + achieved HBM GB/s, final() 500×500×1000spp"   # BASELINE.json
+# rtnw.blocks_for_rank (blocks, the default: 8 x 8 pixel blocks dealt along a Hilbert curve),
 # rtnw.pixels_for_rank (interleaved: rank (ry, rx) of a x b renders x = rx mod a, y = ry mod b)
-# or rtnw.blocks_for_rank (blocks: 8 x 8 pixel blocks dealt along a Hilbert curve)
-LAYOUT = os.environ.get("RTNW_LAYOUT", "interleaved")
+# or rtnw.lattice_blocks_for_rank (lattice: the 8 x 8 blocks on that a x b lattice).  Per-share
+# probe of the final kernel at N = 8: 0.936-0.939 / 0.929-0.932 / 0.929 predicted efficiency
+# (profiles/r05/layouts/)
+LAYOUT = os.environ.get("RTNW_LAYOUT", "blocks")
+
+
+def layout_name(world):
+    if LAYOUT == "interleaved":
+        return "pixel interleave %dx%d" % rtnw.interleave_factors(world)
+    if LAYOUT == "lattice":
+        return "8x8 block lattice %dx%d" % rtnw.interleave_factors(world)
+    return "8x8 blocks dealt along a Hilbert curve"
 
 
 def rank_pixels(nx, ny, rank, world):
@@ -573,7 +586,7 @@ def main():
             "data": f"synthetic: procedural {scene_name}() scene built by the host API (main.cpp builders), "
                     f"counter-RNG samples, seed 2024",
             "config": {"workload": workload, "image": [nx, ny], "spp": spp, "pixels_per_gpu": nx * ny // world,
-                       "rank_layout": ("pixel interleave %dx%d" % rtnw.interleave_factors(world)) if world > 1 else None,
+                       "rank_layout": layout_name(world) if world > 1 else None,
                        "chunk": int(cst["chunk"]),
                        "gather": (("rt_dist_gather (ncclGather)" if native else
                                    f"torch.distributed.gather ({args.dist_backend})") if world > 1 else None),

@@ -54,7 +54,8 @@ def test_rccl_refuses_more_ranks_than_gpus():
 @pytest.mark.parametrize("n,spp", [(2, 8), (8, 2)])
 def test_self_launched_bench_gathers_the_one_gpu_image(tmp_path, n, spp):
     """The driver's N-GPU command shape, rehearsed on one GPU with gloo: N ranks
-    (2 = 2x1, 8 = the 4x2 pixel interleave the 8-GPU node runs), config 5's image
+    (2 and 8, the 8-GPU node's count; bench.py's rank layout: 8x8 blocks dealt along a
+    Hilbert curve, or RTNW_LAYOUT's), config 5's image
     (final() 1000 x 1000), strong scaling, through bench.py's own launcher, its gather
     and rank 0's unpack; the gathered image equals a 1-GPU render of the same job bit
     for bit."""
@@ -67,7 +68,11 @@ def test_self_launched_bench_gathers_the_one_gpu_image(tmp_path, n, spp):
     assert line["n_gpus"] == n and line["scaling"] == "strong"
     assert line["config"]["workload"].startswith("c5: final() 1000x1000")
     assert line["config"]["image"] == [1000, 1000] and line["config"]["spp"] == spp
-    assert line["config"]["rank_layout"] == "pixel interleave %dx%d" % {2: (2, 1), 8: (4, 2)}[n]
+    layout = os.environ.get("RTNW_LAYOUT", "blocks")
+    want = {"blocks": "8x8 blocks dealt along a Hilbert curve",
+            "interleaved": "pixel interleave %dx%d" % {2: (2, 1), 8: (4, 2)}[n],
+            "lattice": "8x8 block lattice %dx%d" % {2: (2, 1), 8: (4, 2)}[n]}[layout]
+    assert line["config"]["rank_layout"] == want
     img = np.load(dump)
 
     import rtnw
