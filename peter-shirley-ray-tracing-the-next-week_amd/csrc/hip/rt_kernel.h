@@ -12,6 +12,7 @@
 #define RT_LDS_BLOCK 1024
 #define RT_LDS_NODE_CAP 1024
 #define RT_LDS_NODE_BYTES (4 * RT_LDS_NODE_CAP * 16)
+#define RT_LDS_NODE_BYTES_MEDIA (14 * RT_LDS_NODE_CAP * 4)   // the media variants' dword planes (rt_device.h RtSplit)
 #define RT_LDS_STACK_BYTES(depth) ((RT_LDS_BLOCK / 64) * (depth) * 64 * 4)
 #define RT_LDS_BUDGET 163840   // LDS bytes per CU (160 KiB)
 
@@ -64,6 +65,8 @@ struct RtKernelArgs {
     const uint32_t *job_xy;   // x | y << 16 per job pixel (image coords)
     uint32_t npix;
     uint32_t nitems;          // npix * nchunks
+    uint32_t ndeep;           // the job's first ndeep pixels are claimed first, all their chunks ...
+    uint32_t ndeep_items;     // ... (ndeep * nchunks items), then the other pixels' (capi.cpp prepare_job)
     uint32_t claim;           // work items per wave-level claim (a multiple of 64) ...
     uint32_t nbig;            // ... for the first nbig claims; the rest (the launch's tail) claim
     uint32_t claim_tail;      //     claim_tail items each, so that waves run dry together

@@ -135,6 +135,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // per wave: the next RT_PRE work items' sample starts, made 64 at a time (refill)
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
+    __shared__ uint2 lds_pre_cp[kBlock / 64][RT_PRE];   // each entry's (sample chunk, job pixel)
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
@@ -145,6 +146,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     CoopSlot *slots = lds_slots[wave];
     uint64_t *pre_key = lds_pre_key[wave];
     float2 *pre_uv = lds_pre_uv[wave];
+    uint2 *pre_cp = lds_pre_cp[wave];
     // the media records are read from LDS (one broadcast read per medium)
     if (kMedia) load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) {
@@ -195,8 +197,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // wave-uniform claim pool, and the pre-made sample starts [pre_head, pre_head + pre_count)
     uint32_t pool_next = 0, pool_end = 0;
     bool exhausted = false;
-    // entry e holds item pre_base + e, of sample chunk pre_c0 (+1 from entry pre_split on)
-    uint32_t pre_head = 0, pre_count = 0, pre_base = 0, pre_c0 = 0, pre_split = 0;
+    // entries [pre_head, pre_head + pre_count) of the wave's pre-made sample starts
+    uint32_t pre_head = 0, pre_count = 0;
 
     // lane state: work item, path, traversal
     uint32_t item = 0xFFFFFFFFu;
@@ -283,9 +285,21 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         const uint32_t n = min(64u, pool_end - pool_next);
         if (kProf) rt_items += n;
         if (lane < n) {
+            // item -> (sample chunk c, job pixel p): the job's first ndeep pixels (capi.cpp:
+            // those whose primary rays enter a dense medium) have all their chunks first,
+            // sample-major, then the other pixels' (RtKernelArgs.ndeep)
             const uint32_t it = pool_next + lane;
-            const uint32_t c = it / A.npix;
-            const uint32_t xy = A.job_xy[it - c * A.npix];
+            uint32_t c, pj;
+            if (it < A.ndeep_items) {
+                c = it / A.ndeep;
+                pj = it - c * A.ndeep;
+            } else {
+                const uint32_t i2 = it - A.ndeep_items, nb = A.npix - A.ndeep;
+                c = i2 / nb;
+                pj = A.ndeep + (i2 - c * nb);
+            }
+            pre_cp[lane] = make_uint2(c, pj);
+            const uint32_t xy = A.job_xy[pj];
             const int x = (int)(xy & 0xFFFFu), j = A.ny - 1 - (int)(xy >> 16);
             const uint64_t K = sample_key(skey, (uint32_t)(j * A.nx + x), c * (uint32_t)A.chunk + A.sample_offset);
             // main.cpp:305-306; A.rnx = RN(1/float(nx)) from the host (div_rn)
@@ -300,9 +314,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         pre_head = 0;
         pre_count = n;
-        pre_base = pool_next;
-        pre_c0 = pool_next / A.npix;
-        pre_split = (pre_c0 + 1) * A.npix - pool_next;
         pool_next += n;
     };
     // retire a finished work item (its sum to the slab), hand the lanes without work
@@ -325,13 +336,13 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const uint32_t rank = lanes_below(need_mask);
             if (need && rank < pre_count) {
                 const uint32_t e = pre_head + rank;
-                item = pre_base + e;
                 pre_k = pre_key[e];
                 pre_cuv = pre_uv[e];
+                const uint2 cp = pre_cp[e];
+                const uint32_t c = cp.x;
+                item = c * A.npix + cp.y;   // the slab slot: [chunk][job pixel]
                 pre_have = true;
                 need = false;
-                // a refill's 64 items cross at most one chunk boundary when npix >= 64
-                const uint32_t c = A.npix >= 64 ? pre_c0 + (e >= pre_split ? 1u : 0u) : item / A.npix;
                 s_cur = (int)(c * (uint32_t)A.chunk);
                 s_end = min(s_cur + A.chunk, A.ns);
                 part = mk(0, 0, 0);
@@ -831,5 +842,5 @@ extern "C" int rt_megakernel_lds_static_actual(void) {
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 + 16 +
-                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8) + RT_LCG_JUMPS * 16) + 256;
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8 + 8) + RT_LCG_JUMPS * 16) + 256;
 }

@@ -167,6 +167,8 @@ struct rt_scene {
     float time0 = 0, time1 = 1;
     // job cache
     std::vector<int32_t> job_tiles;
+    uint32_t job_ndeep = 0;                 // the job's first job_ndeep pixels are the deep ones (prepare_job)
+    std::vector<float> deep_balls;          // dense media's boundary balls (cx, cy, cz, r), rt_scene_create
     uint32_t npix = 0;
     void *job_xy = nullptr, *job_out = nullptr;
     void *slab = nullptr;
@@ -561,6 +563,19 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     s->root = bvh.root;
     s->has_bvh = d->nprims > 0;
     s->nmedia = d->nmedia;
+    // Dense media (mean free path below half the boundary sphere's radius: final()'s
+    // subsurface sphere, not its scene-wide fog): paths that enter one random-walk to the
+    // depth cap, so the job lists the pixels whose primary rays enter one first and the
+    // kernel claims all their samples before the others' (prepare_job): the launch's
+    // last claims then hold few such paths, whose latency chains are its drain.
+    for (int i = 0; i < d->nmedia; i++) {
+        const rt_medium &m = d->media[i];
+        if (m.boundary_count != 1 || !(m.density > 0)) continue;
+        const rt_prim &bp = d->boundary_prims[m.boundary_first];
+        const float R = std::fabs(bp.p[3]);
+        if (bp.kind != RT_PRIM_SPHERE || bp.instance >= 0 || !(1.0f / m.density < 0.5f * R)) continue;
+        s->deep_balls.insert(s->deep_balls.end(), {bp.p[0], bp.p[1], bp.p[2], R});
+    }
     s->bvh_depth = bvh.depth;
     s->nnodes = (int)bvh.node_count();
     s->bvh_width = bvh.width;
@@ -586,8 +601,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     // 60.29 ms on c4, both behind 32-bit entries with the nodes alone.
     {
         s->stack_depth = s->bvh_depth + 1;
-        const long need = (long)RT_LDS_NODE_BYTES + RT_LDS_STACK_BYTES((long)s->stack_depth) +
-                          rt_megakernel_lds_static_bytes();
+        // a scene with media runs a media variant, whose nodes are dword planes (56 KiB)
+        const long node_bytes = d->nmedia > 0 ? (long)RT_LDS_NODE_BYTES_MEDIA : (long)RT_LDS_NODE_BYTES;
+        const long need = node_bytes + RT_LDS_STACK_BYTES((long)s->stack_depth) + rt_megakernel_lds_static_bytes();
         bool want = true;
         if (const char *e = std::getenv("RTNW_LDS_BVH")) want = std::atoi(e) != 0;
         // the budget is this device's LDS per CU (160 KiB on gfx950), and the static part
@@ -644,8 +660,38 @@ static uint64_t slab_budget() {
 // column by column (8 pixels per column), so that ANY 64 consecutive items — a wave
 // claim, wherever it starts — are 8 neighbouring columns of one band (coherent
 // primary rays), also when the tile width is not a multiple of 8 (500 = 62.5 x 8).
-static int prepare_job(rt_scene *s, const int32_t *tiles, int ntiles, int nx, int ny) {
+static bool deep_pixel(const rt_scene *s, const rt_camera_desc *cam, int x, int y, int nx, int ny) {
+    // the pixel centre's primary ray (main.cpp:305-306, camera.h:52-55 without jitter or lens)
+    const float u = (x + 0.5f) / nx, v = (ny - 1 - y + 0.5f) / ny;
+    float o[3], d[3];
+    for (int k = 0; k < 3; k++) {
+        o[k] = cam->origin[k];
+        d[k] = cam->lower_left_corner[k] + u * cam->horizontal[k] + v * cam->vertical[k] - o[k];
+    }
+    for (size_t b = 0; b + 3 < s->deep_balls.size(); b += 4) {
+        const float *c = &s->deep_balls[b];
+        const double oc[3] = {o[0] - (double)c[0], o[1] - (double)c[1], o[2] - (double)c[2]};
+        const double a = (double)d[0] * d[0] + (double)d[1] * d[1] + (double)d[2] * d[2];
+        const double bb = oc[0] * d[0] + oc[1] * d[1] + oc[2] * d[2];
+        const double cc = oc[0] * oc[0] + oc[1] * oc[1] + oc[2] * oc[2] - (double)c[3] * c[3];
+        if (bb * bb - a * cc > 0 && (bb < 0 || cc < 0)) return true;
+    }
+    return false;
+}
+
+static int prepare_job(rt_scene *s, const int32_t *tiles, int ntiles, int nx, int ny, const rt_camera_desc *cam) {
     std::vector<int32_t> key(tiles, tiles + 4 * ntiles);
+    // the deep-first order depends on the camera: its rays' frame joins the cache key
+    bool deep_first = !s->deep_balls.empty();
+    if (const char *e = std::getenv("RTNW_DEEP_FIRST")) deep_first = deep_first && std::atoi(e) != 0;
+    key.push_back(nx);
+    key.push_back(ny);
+    key.push_back(deep_first ? 1 : 0);
+    if (deep_first) {
+        const float *cf[4] = {cam->origin, cam->lower_left_corner, cam->horizontal, cam->vertical};
+        for (const float *f : cf)
+            for (int k = 0; k < 3; k++) { int32_t b; std::memcpy(&b, &f[k], 4); key.push_back(b); }
+    }
     if (key == s->job_tiles && s->job_xy) return RT_OK;
     std::vector<uint32_t> xy, oi;
     uint32_t base = 0;
@@ -661,12 +707,30 @@ static int prepare_job(rt_scene *s, const int32_t *tiles, int ntiles, int nx, in
                 }
         base += (uint32_t)(w * h);
     }
+    // deep pixels first, each group in the band order above (a claim of 64 consecutive
+    // items stays 64 neighbouring pixels of one group)
+    uint32_t ndeep = 0;
+    if (deep_first) {
+        std::vector<uint32_t> dxy, doi, rxy, roi;
+        for (size_t i = 0; i < xy.size(); i++) {
+            const bool deep = deep_pixel(s, cam, (int)(xy[i] & 0xFFFFu), (int)(xy[i] >> 16), nx, ny);
+            (deep ? dxy : rxy).push_back(xy[i]);
+            (deep ? doi : roi).push_back(oi[i]);
+        }
+        ndeep = (uint32_t)dxy.size();
+        if (ndeep == xy.size()) ndeep = 0;   // all deep: one group
+        dxy.insert(dxy.end(), rxy.begin(), rxy.end());
+        doi.insert(doi.end(), roi.begin(), roi.end());
+        xy.swap(dxy);
+        oi.swap(doi);
+    }
     if (s->job_xy) { (void)hipFree(s->job_xy); s->job_xy = nullptr; }
     if (s->job_out) { (void)hipFree(s->job_out); s->job_out = nullptr; }
     s->job_tiles.clear();
     if (int rc = upload(&s->job_xy, xy)) return rc;
     if (int rc = upload(&s->job_out, oi)) return rc;
     s->npix = (uint32_t)xy.size();
+    s->job_ndeep = ndeep;
     s->job_tiles = key;
     return RT_OK;
 }
@@ -684,7 +748,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         return fail(RT_ERR_INVALID, "camera shutter outside the scene's time span (moving-sphere bounds)");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t stream = (hipStream_t)stream_v;
-    if (int rc = prepare_job(s, tiles, ntiles, p->nx, p->ny)) return rc;
+    if (int rc = prepare_job(s, tiles, ntiles, p->nx, p->ny, cam)) return rc;
 
     // Work item = `chunk` samples of one pixel, one by default: short items keep each
     // wave's lanes on neighbouring pixels (a wave deals its claims to lanes as they free
@@ -811,6 +875,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         a.nchunks = (int)(c1 - c0);
         const uint64_t nitems = (uint64_t)s->npix * (c1 - c0);
         a.nitems = (uint32_t)nitems;
+        a.ndeep = s->job_ndeep;
+        a.ndeep_items = (uint32_t)((uint64_t)s->job_ndeep * (c1 - c0));
         // Claim size: up to 512 items per atomic (64 -> 512 is 81.6 -> 76.9 ms on c4:
         // fewer round trips to the one contended counter), at least 8
         // claims per wave so that small jobs still spread over every wave.
