@@ -31,14 +31,15 @@ Prints ONE JSON line (rank 0) with
   roofline: the megakernel is bound by VALU instruction issue.
     achieved = the wave-level VALU instructions of one launch (SQ_INSTS_VALU per
     sample from the committed rocprofv3 pass, profiles/r<NN>/traffic.json, for this
-    very library build) over the kernel's live HIP-event time; peak = the rate 1,024
-    SIMDs x 2.4 GHz (peak engine clock) sustain on THIS kernel's instructions, at the
-    issue cycles per instruction the same build's PMC pass measured: 4 x (SQ_ACTIVE_INST_VALU
-    - SQ_ACTIVE_INST_VALU2) / SQ_INSTS_VALU (one quad-cycle per wave64 instruction, two per
-    transcendental, two instructions in one quad-cycle when they dual-issue:
-    tools/lanes_summary.py).  frac_class_model keeps round 4's per-class model
-    (tools/valu_issue_model.py) for comparison.
-    frac_uniform_2cyc keeps round 1's optimistic roof (every instruction 2 cycles).
+    very library build) over the kernel's live HIP-event time; peak = the hardware
+    ceiling, 1,024 SIMDs x 2.4 GHz (peak engine clock) / 2 cycles per wave64 VALU
+    instruction on SIMD-32 (MI355X_MICROARCH.md), independent of the kernel's own
+    mix; frac = achieved / peak, useful_frac = frac x lane_utilisation.
+    valu_busy_frac = the share of SIMD cycles that issued VALU, at
+    the issue cycles per instruction the same build's PMC pass measured: 4 x
+    (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / SQ_INSTS_VALU (one quad-cycle per
+    wave64 instruction, two instructions in one quad-cycle when they dual-issue:
+    tools/lanes_summary.py) — rounds 4-5 reported it as frac.
     hbm_frac = PMC-measured HBM bytes per launch over the same time vs 8 TB/s;
     cache_served_bytes = SURVEY §8d's byte model.
   cpu_baseline: the reference binary (oracle/_ref/ref_render, compiled from the
@@ -477,7 +478,7 @@ def main():
     prof = read_profile(f"c5_n{nshare}" if cfg == "c5" and nshare > 1 else cfg, sha)
     roof = {"bound": "valu_issue", "achieved": None, "peak": None, "unit": "G wave-VALU-instr/s",
             "frac": None, "traffic": None, "hbm_frac": None, "kernel_ms_avg": avg_kernel_s * 1e3,
-            "frac_uniform_2cyc": None, "valu_issue_cycles_per_instr": None,
+            "frac_uniform_2cyc": None, "valu_busy_frac": None, "valu_issue_cycles_per_instr": None,
             "lane_utilisation": None, "useful_frac": None, "useful_frac_uniform_2cyc": None, "lane_profile": None,
             "lds_level": int(st["lds_level"]), "stack_depth": int(st["stack_depth"]), "scan_groups": int(st["scan_groups"]), "prescan": int(st["prescan"]),
             "batches_per_step": int(st["batches"]),
@@ -506,12 +507,15 @@ def main():
                 "segments_per_wave_iteration": cst["segments"] / max(1.0, cst["wave_iterations"])},
             "note": "the scene is L2/L1-resident: HBM carries ~1% of peak, the kernel is VALU-issue bound "
                     "(DESIGN.md §5c).  achieved = SQ_INSTS_VALU per sample (committed rocprofv3 pass of this "
-                    "library build) x samples / live kernel time; peak = 1024 SIMDs x 2.4 GHz / the issue "
-                    "cycles per instruction the same pass measured, 4 (SQ_ACTIVE_INST_VALU - "
-                    "SQ_ACTIVE_INST_VALU2) / SQ_INSTS_VALU (quad-cycles with dual issue; tools/lanes_summary.py); "
-                    "frac_class_model = round 4's per-class model; frac_uniform_2cyc = the same instructions "
-                    "against 2 cycles each; traffic = PMC HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE); "
-                    "cache_served = SURVEY §8d byte model (node/primitive fetches, mostly L1/L2 hits)"}
+                    "library build) x samples / live kernel time; peak = the hardware ceiling, 1024 SIMDs x "
+                    "2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md), so frac does not "
+                    "depend on how well the kernel issues (since round 6; rounds 4-5 divided by the kernel's "
+                    "own issue cycles per instruction, which is valu_busy_frac now); useful_frac = frac x "
+                    "lane_utilisation (SQ_THREAD_CYCLES_VALU / 64 SQ_ACTIVE_INST_VALU); valu_busy_frac = "
+                    "achieved x 4 (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / SQ_INSTS_VALU / (1024 x 2.4 GHz), "
+                    "the share of SIMD cycles issuing VALU (SURVEY §8d(iii)); traffic = PMC HBM bytes per "
+                    "launch (FETCH_SIZE x 2 + WRITE_SIZE); cache_served = SURVEY §8d byte model (node/primitive "
+                    "fetches, mostly L1/L2 hits)"}
     if prof:
         roof["profile"] = prof["path"]
         roof["profile_matches_library"] = sha in (prof.get("kernel_sha16"), prof.get("lib_sha16"))
@@ -519,16 +523,13 @@ def main():
             vi = prof["valu_insts_per_sample"] * rank_samples
             roof["valu_insts_per_sample"] = prof["valu_insts_per_sample"]
             roof["achieved"] = vi / avg_kernel_s / 1e9
-            roof["frac_uniform_2cyc"] = vi / avg_kernel_s / VALU_PEAK
-            cpi = prof.get("valu_issue_cycles_per_instr")
-            if cpi:
-                # at the 2.4 GHz peak engine clock: the PMC passes saw 2.30-2.36 GHz, so this
-                # frac is a lower bound of the share of issue capacity the kernel uses
-                peak = SIMDS * CLOCK_GHZ * 1e9 / cpi
-                roof["clock_ghz_pmc_pass"] = prof.get("effective_clock_ghz")
-                roof["valu_issue_cycles_per_instr"] = cpi
-                roof["peak"] = peak / 1e9
-                roof["frac"] = vi / avg_kernel_s / peak
+            # the hardware ceiling (MI355X_MICROARCH.md): one wave64 VALU instruction per 2
+            # cycles per SIMD-32 at the 2.4 GHz peak clock, whatever the kernel's own mix
+            # (the fastest opcode measured, v_add_f32 / distinct-source
+            # v_fma_f32, issues in 2.3 cycles: profiles/r06/valu_rates.log)
+            roof["peak"] = VALU_PEAK / 1e9
+            roof["frac"] = vi / avg_kernel_s / VALU_PEAK
+            roof["frac_uniform_2cyc"] = roof["frac"]
         # the share of the issued VALU slots' 64 lanes doing work (committed PMC pass of
         # this build): frac says how full the issue roof is, useful_frac how much of it
         # computes for a lane (the headroom is idle lanes, not issue)
@@ -536,20 +537,16 @@ def main():
         if lanes:
             roof["lane_utilisation"], roof["lane_profile"] = lanes[0], lanes[1]
             if lanes[2] and roof["achieved"] is not None:
-                # the measured issue model (round 5): the VALU's own quad-cycle counters
-                # with dual issue, no instruction classes (tools/lanes_summary.py); the
-                # round-4 class model stays beside it as frac_class_model
-                roof["frac_class_model"] = roof["frac"]
-                roof["valu_issue_cycles_per_instr_class_model"] = roof["valu_issue_cycles_per_instr"]
+                # VALU busy: the issue cycles the kernel's own instructions
+                # took, 4 (ACTIVE - ACTIVE2) / INSTS per instruction (dual issue counted;
+                # tools/lanes_summary.py), over the SIMDs' cycles — how often a SIMD issued
+                # VALU at all, not a fraction of a hardware roof (until round 5 this was `frac`)
                 roof["valu_issue_cycles_per_instr"] = lanes[2]
                 roof["dual_issue_share"] = lanes[3]
-                peak = SIMDS * CLOCK_GHZ * 1e9 / lanes[2]
-                roof["peak"] = peak / 1e9
-                roof["frac"] = roof["achieved"] * 1e9 / peak
+                roof["valu_busy_frac"] = roof["achieved"] * 1e9 * lanes[2] / (SIMDS * CLOCK_GHZ * 1e9)
             if roof["frac"] is not None:
                 roof["useful_frac"] = roof["frac"] * lanes[0]
-            if roof["frac_uniform_2cyc"] is not None:
-                roof["useful_frac_uniform_2cyc"] = roof["frac_uniform_2cyc"] * lanes[0]
+                roof["useful_frac_uniform_2cyc"] = roof["useful_frac"]
         if prof.get("hbm_bytes_per_sample"):
             tr = prof["hbm_bytes_per_sample"] * rank_samples
             roof["traffic"] = tr

@@ -1,10 +1,12 @@
 // examples/render_dist.cpp — the reference's main() (main.cpp:244-336) as a
 // multi-GPU job without PyTorch: one process per GPU, an RCCL communicator
-// (ncclCommInitRank through rt_dist_init), each rank renders its interleaved share
-// of the pixels and ONE ncclGather brings them to rank 0, which writes the PPM
+// (ncclCommInitRank through rt_dist_init), each rank renders its share of the pixels
+// (8 x 8 blocks dealt along a Hilbert curve, rt_rank_tiles, as bench.py splits config 5)
+// and ONE ncclGather brings them to rank 0, which writes the PPM
 // (config 5: final() 1000x1000x1000 over 8 GPUs).
 //
 //   render_dist [--ranks N] [--scene final] [--nx 1000] [--ny 1000] [--ns 1000] [--seed S] [--ppm out.ppm]
+//               [--layout blocks|interleaved|lattice]
 //
 // The launcher forks the N rank processes BEFORE anything touches the GPU (no exec);
 // rank 0 creates the RCCL unique id and passes it to the others through a pipe.
@@ -30,6 +32,7 @@ struct Options {
     std::string scene = "final", ppm = "Test.ppm";
     int nx = 1000, ny = 1000, ns = 1000;   // main.cpp:248-251 (ns as config 5)
     unsigned long long seed = 1;
+    int layout = RT_LAYOUT_BLOCKS;   // rt_dist_set_layout
 };
 
 int run_rank(const Options &o, int rank, int rfd, int wfd) {
@@ -77,6 +80,7 @@ int run_rank(const Options &o, int rank, int rfd, int wfd) {
 
     rt_dist *comm = nullptr;
     if (rt_dist_init(id, rank, o.ranks, device, &comm) != RT_OK) { std::fprintf(stderr, "rt_dist_init: %s\n", rt_last_error()); return 1; }
+    if (rt_dist_set_layout(comm, o.layout) != RT_OK) { std::fprintf(stderr, "rt_dist_set_layout: %s\n", rt_last_error()); return 1; }
     std::vector<float> image(rank == 0 ? size_t(o.nx) * o.ny * 3 : 0);
     rt_stats st;
     const auto t0 = std::chrono::steady_clock::now();
@@ -112,6 +116,8 @@ int main(int argc, char **argv) {
         else if (k == "--ns") o.ns = std::atoi(v.c_str());
         else if (k == "--seed") o.seed = std::strtoull(v.c_str(), nullptr, 0);
         else if (k == "--ppm") o.ppm = v;
+        else if (k == "--layout" && (v == "blocks" || v == "interleaved" || v == "lattice"))
+            o.layout = v == "blocks" ? RT_LAYOUT_BLOCKS : v == "interleaved" ? RT_LAYOUT_INTERLEAVED : RT_LAYOUT_LATTICE;
         else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     }
     if (o.ranks <= 0) {   // one rank per GPU, counted in a child so that this launcher never initialises HIP

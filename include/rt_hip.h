@@ -258,9 +258,10 @@ int rt_math_probe(int fn, const float *a, const float *b, float *out, int64_t n)
 /* ------------------------------------------------ multi-GPU
  * One process per GPU.  The root calls rt_dist_unique_id and hands the 128 bytes to
  * every rank (any side channel); each rank calls rt_dist_init (ncclCommInitRank),
- * renders its share of the pixels — the interleave of rt_rank_pixels: with
- * world = a x b, rank (ry, rx) renders x = rx (mod a), y = ry (mod b), a sub-sampled
- * copy of the whole view — and ONE ncclGather (rccl.h:745) brings the packed shares
+ * renders its share of the pixels — by default 8 x 8 pixel blocks dealt along a
+ * Hilbert curve (rt_rank_tiles, RT_LAYOUT_BLOCKS), or the interleave of rt_rank_pixels:
+ * with world = a x b, rank (ry, rx) renders x = rx (mod a), y = ry (mod b), a
+ * sub-sampled copy of the whole view — and ONE ncclGather (rccl.h:745) brings the packed shares
  * to the root, which unpacks them.  The RNG is keyed by (pixel, sample), so the
  * image is bitwise the 1-GPU image for any rank count.                           */
 #define RT_DIST_ID_BYTES 128
@@ -276,6 +277,21 @@ void rt_interleave_factors(int world, int *a, int *b);
 /* The pixels of `rank` as 1x1 tiles (4 int32 each) in claim order: bands of 8 rows of
  * the rank's lattice, column by column.  Returns the count (tiles == NULL: count only). */
 int64_t rt_rank_pixels(int nx, int ny, int rank, int world, int32_t *tiles, int64_t cap);
+/* How a job's pixels are split over the ranks (rt_rank_tiles, rt_dist_set_layout):
+ *   RT_LAYOUT_BLOCKS       the image's block x block pixel blocks in Hilbert-curve order,
+ *                          block k of the curve to rank k mod world (the default of
+ *                          rt_dist_render and bench.py: every rank's blocks spread over
+ *                          the view, and a wave's 64 work items stay one 8 x 8 block);
+ *   RT_LAYOUT_INTERLEAVED  rt_rank_pixels' pixel interleave;
+ *   RT_LAYOUT_LATTICE      the blocks on the interleave's a x b lattice, row-major.
+ * The pixels come as 1x1 tiles in claim order (each block column by column).  Returns the
+ * count (tiles == NULL: count only), RT_ERR_INVALID for a bad argument or a short buffer;
+ * block <= 0 means RT_LAYOUT_BLOCK.  Replaces main.cpp:299-300's one pixel loop per job. */
+#define RT_LAYOUT_BLOCKS 0
+#define RT_LAYOUT_INTERLEAVED 1
+#define RT_LAYOUT_LATTICE 2
+#define RT_LAYOUT_BLOCK 8
+int64_t rt_rank_tiles(int nx, int ny, int rank, int world, int layout, int block, int32_t *tiles, int64_t cap);
 /* Scatters packed tiles (rt_render_tiles' output layout) into an nx x ny x 3 image. */
 int rt_unpack_tiles(const float *packed, const int32_t *tiles, int64_t ntiles, int nx, int ny, float *image);
 /* The whole rank job: this rank's pixels -> rt_render_tiles -> rt_dist_gather -> on the
@@ -286,6 +302,9 @@ int rt_unpack_tiles(const float *packed, const int32_t *tiles, int64_t ntiles, i
  * and its launcher must stop the peers waiting in the gather. */
 int rt_dist_render(rt_dist *d, rt_scene *s, const rt_camera_desc *cam, const rt_render_params *p, float *image,
                    rt_stats *stats);
+/* The split rt_dist_render uses (RT_LAYOUT_*; RT_LAYOUT_BLOCKS unless set).  Every rank of
+ * a job must set the same layout.  The gathered image is the same for every layout. */
+int rt_dist_set_layout(rt_dist *d, int layout);
 
 /* ----------------------------------------------------- resolve (main.cpp:314-330) */
 /* sqrt gamma + int(255.99*c) + clamp to 255, per channel (main.cpp:316-325). */

@@ -43,6 +43,33 @@ SCENE_DEFAULTS = {
 }
 
 
+def host_libm_pinned():
+    """(pinned, why): whether this host's libm is the one csrc/hip/rt_libm.h restates —
+    glibc 2.35 on an x86-64 CPU with FMA (its sinf ifunc then runs the FMA variant whose
+    constants rt_libm.h was read from).  The oracle calls the host's sinf / asinf / atan2f
+    (texture.h:36, 55; hitable.h:14-19), so a GPU image is the oracle's bit for bit only on
+    such a host; on another the parity bar is north_star's RMS one and the exact-pixel
+    share is reported, not asserted (tests/test_gpu_parity.py assert_exact, smoke())."""
+    import platform
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        libc.gnu_get_libc_version.restype = ctypes.c_char_p
+        ver = libc.gnu_get_libc_version().decode()
+    except (OSError, AttributeError):
+        return False, "the host C library is not glibc"
+    if ver != "2.35":
+        return False, f"host glibc {ver}, rt_libm.h restates 2.35"
+    if platform.machine() != "x86_64":
+        return False, f"host {platform.machine()}, rt_libm.h restates the x86-64 FMA variant"
+    try:
+        flags = open("/proc/cpuinfo").read()
+    except OSError:
+        return False, "no /proc/cpuinfo to check for FMA"
+    if " fma" not in flags:
+        return False, "host CPU without FMA: glibc's sinf runs its non-FMA variant"
+    return True, "glibc 2.35, x86-64 with FMA"
+
+
 def png_rgba(path):
     """Minimal 8-bit non-interlaced PNG decode (test-side; independent of the product's)."""
     import struct

@@ -26,11 +26,9 @@
                             // points, 32 noise scale, 64 unit direction (2, 8: spills, off)
 #endif
 #define RT_INF __builtin_huge_valf()
-// The float transcendentals of the path (texture sines, get_sphere_uv's atan2/asin) as
-// glibc computes them (rt_libm.h, exhaustively pinned); 0: ocml's (A/B, attribution)
-#ifndef RT_GLIBC_MATH
-#define RT_GLIBC_MATH 1
-#endif
+// The float transcendentals of the path (texture sines, get_sphere_uv's atan2/asin) are
+// glibc's (rt_libm.h, exhaustively pinned); ocml's forms, which differ from glibc's on
+// 18-40 % of the call sites' inputs, remain only in rt_math_probe for the comparison.
 
 namespace {
 
@@ -126,25 +124,18 @@ __device__ __forceinline__ double u48x(uint64_t x) {
 // xh * 2^32 + xl (xh < 2^16), so a x = 0xDEECE66D xl + (5 xl + 0xDEECE66D xh) 2^32
 // (mod 2^48): one v_mad_u64_u32 (+ c) and two multiply-adds into the high word, of
 // which only 16 bits are kept — so 16 x 16-bit products suffice (v_mad_u32_u16).
-// RT_LCG_ASM (default 1) spells the four instructions out: from the C form the compiler
-// built the high word as a 64-bit sum (three v_mad_u64_u32, two of them by 0, a 64-bit
-// add and two moves).  The same values either way (the GPU parity tests are bitwise).
-#ifndef RT_LCG_ASM
-#define RT_LCG_ASM 1
-#endif
+// The four instructions are spelled out: from the C form, p = xl * 0xDEECE66D + c and
+// hi = (p >> 32) + 5 xl + 0xDEECE66D xh, the compiler built the high word as a 64-bit sum
+// (three v_mad_u64_u32, two of them by 0, a 64-bit add and two moves; round 4: c4 -0.3 %).
+// The same values either way (the GPU parity tests are bitwise).
 __device__ __forceinline__ uint64_t lcg_step(uint64_t x) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-#if RT_LCG_ASM
     static_assert(kLcgC == 11, "the drand48 increment is the inline constant of v_mad_u64_u32 below");
     uint64_t p, cy;   // cy: the carry-out SGPR pair gfx9 requires (unused)
     uint32_t hi;
     asm("v_mad_u64_u32 %0, %1, %2, %3, 11" : "=v"(p), "=s"(cy) : "v"(xl), "s"(0xDEECE66Du));
     asm("v_mad_u32_u16 %0, %1, 5, %2" : "=v"(hi) : "v"(xl), "v"((uint32_t)(p >> 32)));
     asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(hi) : "v"(xh), "s"(0xE66Du), "v"(hi));
-#else
-    const uint64_t p = (uint64_t)xl * 0xDEECE66Du + kLcgC;
-    const uint32_t hi = (uint32_t)(p >> 32) + xl * 5u + xh * 0xDEECE66Du;
-#endif
     return ((uint64_t)(hi & 0xFFFFu) << 32) | (uint32_t)p;
 }
 // j steps at once: x_{n+j} = A_j x_n + C_j (mod 2^48); jt = (A_j lo, A_j hi, C_j lo, C_j hi)
@@ -152,16 +143,11 @@ typedef unsigned U4j __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint64_t lcg_jump(uint64_t x, U4j jt) {
     const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
     const uint64_t c = ((uint64_t)jt.w << 32) | jt.z;
-#if RT_LCG_ASM
     uint64_t p, cy;
     uint32_t hi;
     asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(p), "=s"(cy) : "v"(xl), "v"(jt.x), "v"(c));   // wraps mod 2^64: 48 bits kept
     asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(hi) : "v"(xl), "v"(jt.y), "v"((uint32_t)(p >> 32)));
     asm("v_mad_u32_u16 %0, %1, %2, %3" : "=v"(hi) : "v"(xh), "v"(jt.x), "v"(hi));
-#else
-    const uint64_t p = (uint64_t)xl * jt.x + c;   // wraps mod 2^64: only 48 bits kept
-    const uint32_t hi = (uint32_t)(p >> 32) + xl * jt.y + xh * jt.x;
-#endif
     return ((uint64_t)(hi & 0xFFFFu) << 32) | (uint32_t)p;
 }
 // Jumps of 0 .. RT_LCG_JUMPS - 1 steps: a cooperative round's candidate t of an owner
@@ -445,8 +431,8 @@ struct Hit { V3 p, n; float u, v; int mat; };
 
 // get_sphere_uv (hitable.h:14-19): float atan2/asin, then the double M_PI arithmetic.
 __device__ __forceinline__ void sphere_uv(V3 p, float &u, float &v) {
-    const float phi = RT_GLIBC_MATH ? rt_atan2f(p.z, p.x) : atan2f(p.z, p.x);
-    const float theta = RT_GLIBC_MATH ? rt_asinf(p.y) : asinf(p.y);
+    const float phi = rt_atan2f(p.z, p.x);
+    const float theta = rt_asinf(p.y);
     u = (float)(1 - ((double)phi + 3.14159265358979323846) / (2 * 3.14159265358979323846));
     v = (float)(((double)theta + 3.14159265358979323846 / 2) / 3.14159265358979323846);
 }
@@ -592,8 +578,7 @@ __device__ __forceinline__ int tex_leaf(const RtKernelArgs &A, int ti, V3 p, flo
         t1 = A.texs[ti * 2 + 1];
         const int kind = fbits(t0.x);
         if (kind != RT_TEX_CHECKER) return kind;
-        float sines = RT_GLIBC_MATH ? rt_sinf(10 * p.x) * rt_sinf(10 * p.y) * rt_sinf(10 * p.z)
-                                    : sinf(10 * p.x) * sinf(10 * p.y) * sinf(10 * p.z);
+        float sines = rt_sinf(10 * p.x) * rt_sinf(10 * p.y) * rt_sinf(10 * p.z);
         ti = (sines < 0) ? fbits(t0.z) : fbits(t0.y);
     }
     return -1;
@@ -626,10 +611,7 @@ __device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, fl
 // -o/d, duplicated into packed pairs for v_pk_fma_f32.
 // LDS nodes (LdsNodes::load_signed): lx/ly/lz are the byte offsets of the ray's
 // near planes in the axis' plane (+4 when the direction is negative: hi before lo).
-#ifndef RT_LDS_SIGNED
-#define RT_LDS_SIGNED 1
-#endif
-// kSplit = 1 (RT_LDS_SIGNED layouts): every value of a node in a plane of its own, one dword
+// kSplit = 1: every value of a node in a plane of its own, one dword
 // per node — 14 planes of RT_LDS_NODE_CAP dwords: the child references c0, c1, then x-lo,
 // x-hi, y-lo, y-hi, z-lo, z-hi of child 0 and child 1 in turn (RtSplit) — so the values of
 // both children for one axis and side are one plane (4 KiB) apart and load as one
@@ -641,8 +623,13 @@ __device__ __forceinline__ V3 tex_value_leaf(const RtKernelArgs &A, int kind, fl
 // the LDS-active cycles); blocks of 32 nodes conflict the same, an odd 15-dword node stride
 // conflicts least (0.20) and was slower on final() (+0.45 %): profiles/r05/lds_layouts/.
 enum RtSplit { RS_C0 = 0, RS_C1 = 1, RS_XLO = 2, RS_XHI = 4, RS_YLO = 6, RS_YHI = 8, RS_ZLO = 10, RS_ZHI = 12, RS_PLANES = 14 };
+// The LDS node layout of a kernel variant: dword planes for the media variants' BVH2 in
+// LDS (final()), float4 planes otherwise (the layout each measured fastest)
+__host__ __device__ constexpr int rt_lds_split(int mode, int feat, int width) {
+    return (mode == 1 && (feat & RT_FEAT_MEDIA) != 0 && width == 2) ? 1 : 0;
+}
 #define RT_SPLIT_PB (RT_LDS_NODE_CAP * 4)   // bytes per dword plane
-// node bytes of the LDS layout (the host sizes the LDS by the larger, float4 one)
+// node bytes of the LDS layout (the host asks rt_lds_need_bytes for its scene's variant)
 template <int kSplit>
 constexpr uint32_t lds_node_bytes() { return kSplit ? RS_PLANES * RT_SPLIT_PB : RT_LDS_NODE_BYTES; }
 // an interior node's reference: its byte offset in a plane
@@ -718,20 +705,16 @@ struct GlobalNodes {
     __device__ __forceinline__ const float4 *ptr8(uint32_t n) const { return p + n * 16; }
     __device__ __forceinline__ const float4 *ptr8q(uint32_t n) const { return p + n * 8; }
 };
-// LDS planes, per axis (RT_LDS_SIGNED): plane 0 holds the child references (first,
+// LDS planes, per axis: plane 0 holds the child references (first,
 // so that their read needs no address add: the LDS base fits the immediate offset),
 // plane 1 + a (lo0, hi0, lo1, hi1) of axis a for both children.  A lane reads its near planes at
 // +0 or +4 by the sign of its direction (Slab::lx..lz) and its far planes at the
 // other word: near/far come out of the load, not out of a min and a max per axis
-// and child (12 VALU per node step for 6 address adds).  Without RT_LDS_SIGNED the
-// planes are the node's 4 float4 (rt_layout.h).
+// and child (12 VALU per node step for 6 address adds; the node's 4 float4 read by
+// four ds_read_b128, round 2: c4 56.95 -> 55.68 ms).
 template <int kSplit = 0>
 struct LdsNodes {   // node references are byte offsets (n * 16, kSplit: n * 4) into the planes
     const LdsF4 *p;
-    __device__ __forceinline__ void load2(uint32_t n, float4 &b0, float4 &b1, float4 &b2, float4 &cf) const {
-        const LdsF4 *N = (const LdsF4 *)((__attribute__((address_space(3))) const char *)p + n);
-        b0 = f4(N[0]); b1 = f4(N[RT_LDS_NODE_CAP]); b2 = f4(N[2 * RT_LDS_NODE_CAP]); cf = f4(N[3 * RT_LDS_NODE_CAP]);
-    }
     // the six plane offsets become LDS addresses once per round, opaque to the
     // compiler, which would otherwise re-split base + plane + sign per node step
     // (11 address adds per node instead of 6)
@@ -779,23 +762,12 @@ struct LdsNodes {   // node references are byte offsets (n * 16, kSplit: n * 4) 
 
 // The traversal stack: one column per lane, [depth][lane] (a wave's push or pop is one
 // conflict-free ds_write_b32 / ds_read_b32), addressed by the depth `sp` with one shift-add.
-// RT_SP_BYTES = 1 (A/B): sp holds the byte offset (depth x 256) instead, so the address is
-// one fast add — but the conditional +-256 steps become selects (4-cycle VALU) where the
-// depth steps were carry-in adds, and c4's variant spilled 8 B.
-#ifndef RT_SP_BYTES
-#define RT_SP_BYTES 0
-#endif
-#if RT_SP_BYTES
-#define RT_SP_UNIT 256
-__device__ __forceinline__ uint32_t &stk_at(uint32_t *stk, int sp) {
-    return *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(stk) + sp);
-}
-#else
+// (sp as a byte offset, depth x 256, makes the address one add but turns the conditional
+// +-1 steps, carry-in adds, into selects: c4 51.54 -> 51.68 ms with 8 B spilled, round 5.)
 #define RT_SP_UNIT 1
 __device__ __forceinline__ uint32_t &stk_at(uint32_t *stk, int sp) {   // one shift-add per address
     return *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(stk) + ((uint32_t)sp << 8));
 }
-#endif
 
 // 8-wide node step's tail: the nearest hit child (the first one in slot order on
 // ties) is the next node, the other hit children are pushed in reverse slot order.
@@ -827,7 +799,7 @@ __device__ __forceinline__ uint32_t wide8_tail(const float k[8], const uint32_t 
 template <int kWidth, class Nodes>
 __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, const Slab &s, float best_t, uint32_t *stk,
                                               int &sp) {
-    if constexpr (kWidth == 2 && RT_LDS_SIGNED && !std::is_same<Nodes, GlobalNodes>::value) {
+    if constexpr (kWidth == 2 && !std::is_same<Nodes, GlobalNodes>::value) {
         F2 nx, ny, nz, fx, fy, fz;
         uint32_t c0, c1;
         src.load_signed(node, s, nx, ny, nz, fx, fy, fz, c0, c1);
@@ -1294,9 +1266,6 @@ __device__ __forceinline__ void scan_keep(float t, int key, int q, bool in, int 
 }
 // plane_t without branches: the in-plane coordinates are computed for every t (an
 // out-of-range t is replaced by RT_INF either way), so one select decides the hit
-#ifndef RT_SCAN_PAIRS
-#define RT_SCAN_PAIRS 1
-#endif
 template <bool kCount>
 __device__ __forceinline__ int scan_rects(const ConstF4 *P, int q, int n, float oa, float da, float oi, float di,
                                           float oj, float dj, float tmin, bool in, int ck, ScanBest &b, Counters &cnt) {
@@ -1308,14 +1277,12 @@ __device__ __forceinline__ int scan_rects(const ConstF4 *P, int q, int n, float 
         scan_keep<kCount>(miss ? RT_INF : t, -1 - fbits(mm.w), i, in, ck, b, cnt);
     };
     const ConstF4 *p = P + 4 * q;   // a running record pointer: no per-primitive address arithmetic
-    if (RT_SCAN_PAIRS) {
-        // two records per scalar-load wait (scalar loads return out of order, so
-        // every use waits for all of them: a pair halves the waits)
-        for (; q + 1 < e; q += 2, p += 8) {
-            const F4v g0a = p[0], mma = p[1], g0b = p[4], mmb = p[5];
-            test(g0a, mma, q);
-            test(g0b, mmb, q + 1);
-        }
+    // two records per scalar-load wait (scalar loads return out of order, so
+    // every use waits for all of them: a pair halves the waits)
+    for (; q + 1 < e; q += 2, p += 8) {
+        const F4v g0a = p[0], mma = p[1], g0b = p[4], mmb = p[5];
+        test(g0a, mma, q);
+        test(g0b, mmb, q + 1);
     }
     if (q < e) test(p[0], p[1], q);
     return e;
@@ -1349,13 +1316,9 @@ __device__ __forceinline__ void scan_group(const ConstF4 *P, int q, int kinds, i
 // volatile read at each use, so the compiler neither hoists them into registers held
 // across the persistent loop (where they were spilled to scratch) nor folds them back.
 typedef LogConsts MediaConsts;   // log_f64's coefficients
-// how the media stage reads them: 0 the round-4 way (only 0.2 from LDS; with the glibc sine
-// inlined it spills, c4 +1.4 %), 1 five volatile reads, 2 one record copy read at the use
-// (1 and 2 measure alike: profiles/r05/ab_log_consts_ocml_r04.log; 0.2 and -1/6 alone
-// from LDS spill too)
-#ifndef RT_LOG_CONSTS
-#define RT_LOG_CONSTS 2
-#endif
+// The media stage reads them as one record copy at the use (five volatile reads measure
+// alike; only 0.2 from LDS, the round-4 way, spilled with the glibc sine inlined, c4 +1.4 %:
+// profiles/r05/ab_log_consts_ocml_r04.log).
 typedef __attribute__((address_space(3))) const volatile MediaConsts LdsMediaConsts;
 // constant_medium::hit for every medium after the surface search
 // (constant_medium.h:26-50): the boundary's entry/exit, clipped to [t_min, best]
@@ -1431,13 +1394,9 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     r1 = r1 < 0 ? 0.f : r1;
     const float distance_inside_boundary = (r2 - r1) * dlen;
     const float neg_inv_density = __int_as_float(md.z);   // -(1/density), host-side
-#if RT_LOG_CONSTS == 0   // round 4's: 0.2 from LDS, the rest immediates
-    const LogConsts lc{1.0 / 7, -1.0 / 6, mc->c02, -0.25, 1.0 / 3};
-#elif RT_LOG_CONSTS == 1  // each coefficient by its own volatile LDS read
+#if !defined(__HIP_DEVICE_COMPILE__)   // (the host pass never runs device code)
     const LogConsts lc{mc->c07, mc->c06, mc->c02, mc->c025, mc->c03};
-#elif !defined(__HIP_DEVICE_COMPILE__)   // (the host pass never runs device code)
-    const LogConsts lc{mc->c07, mc->c06, mc->c02, mc->c025, mc->c03};
-#else                     // one copy of the record through an opaque LDS address: read at the use, vectorised
+#else                                   // one copy of the record through an opaque LDS address: read at the use
     uint32_t mca = (uint32_t)(size_t)mc;
     asm volatile("" : "+v"(mca));
     const LogConsts lc = *(__attribute__((address_space(3))) const LogConsts *)(size_t)mca;
@@ -1532,7 +1491,7 @@ __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool re
     if (kCount && noisy) cnt.noise++;
     const float turb = coop_turb(noisy, scale(nscale, hr.p), A.ranvec, A.perm, slots, lane);   // perlin.h:64-74
     if (noisy) {                                                                               // texture.h:52-56
-        const float sv = 1 + (RT_GLIBC_MATH ? rt_sinf(nscale * hr.p.x + 5 * turb) : sinf(nscale * hr.p.x + 5 * turb));
+        const float sv = 1 + rt_sinf(nscale * hr.p.x + 5 * turb);
         const float h = 0.5f * 1;
         st.tv = mk(sv * h, sv * h, sv * h);
     }

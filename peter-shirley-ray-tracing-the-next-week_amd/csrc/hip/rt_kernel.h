@@ -94,3 +94,6 @@ extern "C" hipError_t rt_megakernel_occupancy(int *blocks_per_cu, int mode, int 
 extern "C" int rt_megakernel_lds_static_bytes(void);
 // the largest static LDS (bytes) the compiler gave any LDS-BVH variant (hipFuncGetAttributes), 0 if unknown
 extern "C" int rt_megakernel_lds_static_actual(void);
+// LDS bytes per workgroup of the BVH2-in-LDS variant a scene with `features` (RT_FEAT_*)
+// runs, with traversal stacks of `stack_depth` entries (rt_kernel.hip)
+extern "C" long rt_lds_need_bytes(int features, int stack_depth);

@@ -41,13 +41,9 @@ namespace {
 // argument; 4 -> <= 128 VGPRs -> 16 waves per CU).  5 waves (96 VGPRs) spill 63
 // VGPRs and run 24% slower.
 
-// Shade once this many lanes of a wave have their closest hit (see stage 3).
-// partial sums in the slab: rgb, 12 B per work item (RT_SLAB_F4=1: 16-B records, A/B only)
-#if defined(RT_SLAB_F4) && RT_SLAB_F4
-#define RT_SLAB_FLOATS 4
-#else
+// partial sums in the slab: rgb, 12 B per work item (16-B float4 records until round 3)
 #define RT_SLAB_FLOATS 3
-#endif
+// Shade once this many lanes of a wave have their closest hit (see stage 3).
 #ifndef RT_READY_BATCH
 #define RT_READY_BATCH 48
 #endif
@@ -64,11 +60,6 @@ namespace {
 #define RT_DRY_LANES 16
 #endif
 
-
-// The LDS node layout of the media variants (rt_device.h RtSplit): 1 dword planes, 0 float4 planes
-#ifndef RT_LDS_SPLIT_MEDIA
-#define RT_LDS_SPLIT_MEDIA 1
-#endif
 
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
@@ -92,27 +83,19 @@ enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
 //      at launch; node steps read them with ds_read_b128), stacks of the scene's depth;
 //   2  flat scan of the primitive groups (rt_layout.h rt_dgroup), primitives in LDS,
 //      no BVH and no stack: scenes of at most RT_SCAN_MAX primitives.
-// Kernel arguments re-read each loop iteration (RT_KARGS_RELOAD): the persistent
+// Kernel arguments re-read each loop iteration: the persistent
 // loop reads ~40 uniform arguments; held in SGPRs across it they overflowed the 102
 // addressable SGPRs, which the compiler spilled into the lanes of a VGPR (v_writelane
 // at entry, a v_readlane — a VALU issue — per use).  Through a kernarg pointer that is
 // made opaque at the top of every iteration they are scalar loads (SMEM, scalar
 // cache) at their first use in the iteration instead (c4 53.01 -> 52.24 ms, c3
 // 45.55 -> 45.44 ms; SGPR spills 36 -> 0).
-#ifndef RT_KARGS_RELOAD
-#define RT_KARGS_RELOAD 1
-#endif
 typedef __attribute__((address_space(4))) const RtKernelArgs KArgs;
 __device__ __forceinline__ KArgs *opaque_kargs(KArgs *p) {
-#if RT_KARGS_RELOAD
     asm volatile("" : "+s"(p));
-#endif
     return p;
 }
 
-#ifndef RT_MERGE_SEG
-#define RT_MERGE_SEG 1
-#endif
 template <bool kCount, bool kProf, int kWidth, int kFeat, int kMode>
 __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_SIMD) void rt_megakernel(RtKernelArgs A_param) {
     (void)A_param;   // read through ka (the same bytes: the kernarg segment holds A_param at offset 0)
@@ -124,7 +107,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
     // the LDS node layout (rt_device.h RtSplit): dword planes in the media variants (final()),
     // float4 planes otherwise, as each measured fastest
-    constexpr int kSplit = (kLds && kMedia && RT_LDS_SIGNED && kWidth == 2) ? RT_LDS_SPLIT_MEDIA : 0;
+    constexpr int kSplit = rt_lds_split(kMode, kFeat, kWidth);
     constexpr int kBlock = kLds ? RT_LDS_BLOCK : RT_BLOCK;
     __shared__ uint32_t lds_stack[kMode ? 1 : RT_BLOCK / 64][kMode ? 1 : (kWidth >= 8 ? RT_STACK_DEPTH_W8 : RT_STACK_DEPTH)][64];
     __shared__ CoopSlot lds_slots[kBlock / 64][64];
@@ -175,18 +158,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 P[RS_ZLO * C] = b1.x; P[(RS_ZLO + 1) * C] = b2.z; P[RS_ZHI * C] = b1.y; P[(RS_ZHI + 1) * C] = b2.w;
                 continue;
             }
-#if RT_LDS_SIGNED
             // the references, then per-axis planes (LdsNodes::load_signed): (lo0, hi0, lo1, hi1) of x, y, z
             lds_dyn[i] = cf;
             lds_dyn[i + RT_LDS_NODE_CAP] = make_float4(b0.x, b0.y, b1.z, b1.w);
             lds_dyn[i + 2 * RT_LDS_NODE_CAP] = make_float4(b0.z, b0.w, b2.x, b2.y);
             lds_dyn[i + 3 * RT_LDS_NODE_CAP] = make_float4(b1.x, b1.y, b2.z, b2.w);
-#else
-            lds_dyn[i] = b0;
-            lds_dyn[i + RT_LDS_NODE_CAP] = b1;
-            lds_dyn[i + 2 * RT_LDS_NODE_CAP] = b2;
-            lds_dyn[i + 3 * RT_LDS_NODE_CAP] = cf;
-#endif
         }
     }
     __syncthreads();
@@ -230,13 +206,6 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     uint64_t rt_exhaust = 0;
     uint32_t rt_items = 0;   // work items this wave claimed (kProf)
     auto mark = [&](int k) {
-#ifdef RT_ASM_MARKS
-        if (k == 0) asm volatile("; @@MARK 0" ::: "memory");
-        else if (k == 1) asm volatile("; @@MARK 1" ::: "memory");
-        else if (k == 2) asm volatile("; @@MARK 2" ::: "memory");
-        else if (k == 3) asm volatile("; @@MARK 3" ::: "memory");
-        else asm volatile("; @@MARK 4" ::: "memory");
-#endif
         if (kProf) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             prof[k] += now - stamp;
@@ -374,7 +343,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             }
         }
     };
-    // seg: begin the segment here (else the caller does, RT_MERGE_SEG)
+    // seg: begin the segment here (else the caller does)
     auto camera_finish = [&](bool starting, float cu_, float cv_, V3 disk, bool seg = true) {
         if (starting) {
             const CamView C = load_camera(lds_cam);
@@ -486,7 +455,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
                     Slab sl = make_slab<kSplit>(r, A.tmin);
                     uint32_t pleaf;
-                    if constexpr (kLds && RT_LDS_SIGNED && kWidth == 2) lnodes.prepare(sl);
+                    if constexpr (kLds && kWidth == 2) lnodes.prepare(sl);
                     if constexpr (kLds)
                         pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(lnodes, node, sl, best_t, stk, sp, cnt, dry);
                     else
@@ -585,8 +554,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         mark(3);
         // a scattered path and a new camera sample (disjoint lanes: a lane that started
         // a sample this iteration was idle, not ready) begin their next segment in ONE
-        // place (RT_MERGE_SEG): the compiler otherwise materialises the segment state in
-        // both divergent branches
+        // place: the compiler otherwise materialises the segment state in both divergent
+        // branches
         bool seg = false;
         if (ready && !ends) {
             const ShadeOut so = shade_finish(A, ready, have, r, rd, hr, st, pt, g);
@@ -594,35 +563,15 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 beta = mul(beta, so.att);
                 r = so.ray;
                 ++depth;
-                if (RT_MERGE_SEG) seg = true; else begin_segment();
+                seg = true;
             } else {
                 end_path(mul(beta, so.emitted));
             }
         }
         mark(4);
-        camera_finish(starting, cu_, cv_, pt, !RT_MERGE_SEG);
-        if (RT_MERGE_SEG && (seg || starting)) begin_segment();
+        camera_finish(starting, cu_, cv_, pt, false);
+        if (seg || starting) begin_segment();
         mark(3);
-#ifdef RT_PROBE_VALU
-#if RT_PROBE_VALU == 1
-#define RT_PROBE_OP "v_add_f32 %0, %0, %1"
-#elif RT_PROBE_VALU == 2
-#define RT_PROBE_OP "v_max_f32 %0, %0, %1"
-#else
-#define RT_PROBE_OP "v_fma_f32 %0, %0, %1, %1"
-#endif
-        {   // timing probe only: 64 independent extra VALU instructions of one opcode per
-            // wave iteration, on registers that feed nothing (in-situ costs)
-            float q0 = (float)lane, q1 = q0 + 1.f, q2 = q0 + 2.f, q3 = q0 + 3.f;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                asm volatile(RT_PROBE_OP : "+v"(q0) : "v"(q1));
-                asm volatile(RT_PROBE_OP : "+v"(q1) : "v"(q2));
-                asm volatile(RT_PROBE_OP : "+v"(q2) : "v"(q3));
-                asm volatile(RT_PROBE_OP : "+v"(q3) : "v"(q0));
-            }
-        }
-#endif
     }
     if (kProf && lane == 0) {
         // the scatter branches' cycles count in the shade stage too
@@ -729,8 +678,16 @@ __global__ __launch_bounds__(256) void rt_math_probe_kernel(int fn, const float 
     out[i] = r;
 }
 
+#ifdef RT_KNOB_CHECK
+// tests/test_device_knobs.py: a device-only build of final()'s variant (BVH2 in LDS, media)
+// and cornell_box's (flat scan, instances), with a non-default value of one compile-time
+// knob — seconds instead of the whole variant set's minute — so no knob value goes uncompiled.
+template __global__ void rt_megakernel<false, false, 2, RT_FEAT_MEDIA, 1>(RtKernelArgs);
+template __global__ void rt_megakernel<false, false, 2, RT_FEAT_INST, 2>(RtKernelArgs);
+#endif
 }  // namespace
 
+#ifndef RT_KNOB_CHECK
 extern "C" hipError_t rt_launch_math_probe(int fn, const float *a, const float *b, float *out, int n, hipStream_t stream) {
     hipLaunchKernelGGL(rt_math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, fn, a, b, out, n);
     return hipGetLastError();
@@ -743,8 +700,7 @@ static hipError_t launch_one(const RtKernelArgs *a, int grid, hipStream_t stream
     size_t dyn = 0;
     if (kLds == 1) {
         // the variant's node layout (rt_megakernel's kSplit): dword planes need 56 KiB, float4 planes 64
-        constexpr int kSplitL = ((kFeat & RT_FEAT_MEDIA) != 0 && RT_LDS_SIGNED && kWidth == 2) ? RT_LDS_SPLIT_MEDIA : 0;
-        dyn = lds_node_bytes<kSplitL>() + RT_LDS_STACK_BYTES(a->stack_depth);
+        dyn = lds_node_bytes<rt_lds_split(kLds, kFeat, kWidth)>() + RT_LDS_STACK_BYTES(a->stack_depth);
         // Dynamic LDS above the default limit: the attribute (the most any scene can
         // ask for) is set once per device and variant, recorded in an atomic bit mask
         // (thread-safe; calling hipFuncSetAttribute before every launch cost ~0.6 ms
@@ -774,6 +730,19 @@ static hipError_t launch_variant(const RtKernelArgs *a, int grid, int mode, hipS
     if (mode == 1) return launch_one<true, false, kWidth, kFeat, kLds>(a, grid, stream);
     if (mode == 2) return launch_one<false, true, kWidth, kFeat, kLds>(a, grid, stream);
     return launch_one<false, false, kWidth, kFeat, kLds>(a, grid, stream);
+}
+
+// The compiled variant that runs a scene's features (launch_features below).
+static int variant_of(int features) {
+    switch (features) {
+    case 0:
+    case RT_FEAT_MEDIA: return RT_FEAT_MEDIA;
+    case RT_FEAT_INST: return RT_FEAT_INST;
+    case RT_FEAT_INST | RT_FEAT_MEDIA: return RT_FEAT_INST | RT_FEAT_MEDIA;
+    case RT_FEAT_CHECKER:
+    case RT_FEAT_CHECKER | RT_FEAT_PRESCAN: return RT_FEAT_CHECKER | RT_FEAT_PRESCAN;
+    default: return RT_FEAT_ALL;
+    }
 }
 
 template <int kLds>
@@ -839,8 +808,30 @@ extern "C" int rt_megakernel_lds_static_actual(void) {
                     std::max(lds_static_of<RT_FEAT_CHECKER | RT_FEAT_PRESCAN>(), lds_static_of<RT_FEAT_ALL>()));
 }
 
+// LDS bytes per workgroup the BVH2-in-LDS variant for `features` needs with stacks of
+// `stack_depth` entries: its static arrays (the compiled kernel's own count, or the
+// estimate below where no HIP device answers), its node layout (rt_lds_split: 56 KiB of
+// dword planes for the media variants, 64 KiB of float4 planes otherwise) and the
+// stacks — what launch_one asks for, so the host's eligibility check and the launch agree.
+extern "C" int rt_megakernel_lds_static_bytes(void);
+extern "C" long rt_lds_need_bytes(int features, int stack_depth) {
+    const int v = variant_of(features);
+    int stat = 0;
+    switch (v) {
+    case RT_FEAT_MEDIA: stat = lds_static_of<RT_FEAT_MEDIA>(); break;
+    case RT_FEAT_INST: stat = lds_static_of<RT_FEAT_INST>(); break;
+    case RT_FEAT_INST | RT_FEAT_MEDIA: stat = lds_static_of<RT_FEAT_INST | RT_FEAT_MEDIA>(); break;
+    case RT_FEAT_CHECKER | RT_FEAT_PRESCAN: stat = lds_static_of<RT_FEAT_CHECKER | RT_FEAT_PRESCAN>(); break;
+    default: stat = lds_static_of<RT_FEAT_ALL>(); break;
+    }
+    stat = std::max(stat, rt_megakernel_lds_static_bytes());
+    const long nodes = rt_lds_split(1, v, 2) ? lds_node_bytes<1>() : lds_node_bytes<0>();
+    return (long)stat + nodes + (long)RT_LDS_STACK_BYTES((long)stack_depth);
+}
+
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 + 16 +
                  (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8 + 8) + RT_LCG_JUMPS * 16) + 256;
 }
+#endif  // RT_KNOB_CHECK

@@ -32,12 +32,8 @@
 
 #if defined(__HIPCC__)
 #define RT_LIBM_FN __host__ __device__ __forceinline__
-#ifndef RTL_LARGE_FN
 #define RTL_LARGE_FN __host__ __device__ __forceinline__
-#endif
-#ifndef RTL_SINF_FN
 #define RTL_SINF_FN __host__ __device__ __forceinline__
-#endif
 #else
 #define RT_LIBM_FN static inline
 #define RTL_LARGE_FN static inline

@@ -181,6 +181,17 @@ struct rt_scene {
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
 
+// The kernel features (RT_FEAT_*) a scene's launches carry code for: the launcher runs the
+// smallest compiled variant covering them (rt_kernel.hip launch_features).  RTNW_FEAT_ALL=1
+// runs the all-feature variant (the one the wide BVHs use): A/B runs only.
+static int scene_features(const rt_scene *s) {
+    if (const char *e = std::getenv("RTNW_FEAT_ALL"))
+        if (std::atoi(e)) return RT_FEAT_ALL;
+    return (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
+           (s->has_checker ? RT_FEAT_CHECKER : 0) | (s->nprescan > 0 ? RT_FEAT_PRESCAN : 0) |
+           (s->nmedia > 0 ? RT_FEAT_MEDIA : 0);
+}
+
 extern "C" {
 
 const char *rt_last_error(void) { return g_err.c_str(); }
@@ -495,7 +506,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         // constant: its color in the unused albedo slots, flag 2 (shade_begin then reads
         // no texture record: one dependent load fewer per shade)
         const bool textured = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_ISOTROPIC || m.kind == RT_MAT_DIFFUSE_LIGHT;
-        if (RT_MAT_CONST_TEX && textured && m.texture >= 0 && m.texture < d->ntextures &&
+        if (textured && m.texture >= 0 && m.texture < d->ntextures &&
             d->textures[m.texture].kind == RT_TEX_CONSTANT) {
             for (int k = 0; k < 3; k++) o.albedo[k] = d->textures[m.texture].color[k];
             o.flags |= 2;
@@ -601,9 +612,8 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     // 60.29 ms on c4, both behind 32-bit entries with the nodes alone.
     {
         s->stack_depth = s->bvh_depth + 1;
-        // a scene with media runs a media variant, whose nodes are dword planes (56 KiB)
-        const long node_bytes = d->nmedia > 0 ? (long)RT_LDS_NODE_BYTES_MEDIA : (long)RT_LDS_NODE_BYTES;
-        const long need = node_bytes + RT_LDS_STACK_BYTES((long)s->stack_depth) + rt_megakernel_lds_static_bytes();
+        // the variant this scene launches (its static arrays and node layout: rt_lds_need_bytes)
+        const long need_actual = rt_lds_need_bytes(scene_features(s), s->stack_depth);
         bool want = true;
         if (const char *e = std::getenv("RTNW_LDS_BVH")) want = std::atoi(e) != 0;
         // the budget is this device's LDS per CU (160 KiB on gfx950), and the static part
@@ -613,8 +623,6 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
         if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess ||
             lds_cu <= 0)
             lds_cu = 0;
-        const long stat = std::max<long>(rt_megakernel_lds_static_bytes(), rt_megakernel_lds_static_actual());
-        const long need_actual = need - rt_megakernel_lds_static_bytes() + stat;
         s->lds_nodes = want && !s->scan && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
                        s->nnodes <= RT_LDS_NODE_CAP &&
                        need_actual <= std::min<long>(RT_LDS_BUDGET, lds_cu);
@@ -637,17 +645,13 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
 }
 
 // Small claims per wave at the end of a launch (render_tiles' claim sizes).
-#ifndef RT_TAIL_CLAIMS
 #define RT_TAIL_CLAIMS 32
-#endif
 
 // Partial-sum slab budget per launch (bytes; env RTNW_SLAB_BUDGET overrides, for tests).
 // A job whose slab would be larger runs as several launches over sample batches.
 // 16 GiB of the 288 GiB HBM: config 5 on one GPU (1e9 samples, 12 GB) is one launch,
 // one launch-end drain; 8 GiB made it two.
-#ifndef RT_SLAB_BUDGET
 #define RT_SLAB_BUDGET (16ull << 30)
-#endif
 static uint64_t slab_budget() {
     if (const char *e = std::getenv("RTNW_SLAB_BUDGET")) {
         const unsigned long long v = std::strtoull(e, nullptr, 10);
@@ -815,11 +819,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.nprescan = s->nprescan;
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
-    a.features = (s->ninstances > 0 ? RT_FEAT_INST : 0) | (s->has_uv ? RT_FEAT_UV : 0) |
-                 (s->has_checker ? RT_FEAT_CHECKER : 0) | (s->nprescan > 0 ? RT_FEAT_PRESCAN : 0) |
-                 (s->nmedia > 0 ? RT_FEAT_MEDIA : 0);
-    // RTNW_FEAT_ALL=1 runs the all-feature variant (the one the wide BVHs use): A/B runs only
-    if (const char *e = std::getenv("RTNW_FEAT_ALL")) if (std::atoi(e)) a.features = RT_FEAT_ALL;
+    a.features = scene_features(s);
     for (int k = 0; k < 3; k++) {
         a.org[k] = cam->origin[k];
         a.llc[k] = cam->lower_left_corner[k];

@@ -1,6 +1,7 @@
 // dist.cpp — the multi-GPU half of the C ABI (include/rt_hip.h, "multi-GPU"):
-// one process per GPU, RCCL communicator (ncclCommInitRank), the pixel interleave
-// that gives every rank a sub-sampled copy of the view, and ONE
+// one process per GPU, RCCL communicator (ncclCommInitRank), the rank shares (by default
+// 8 x 8 pixel blocks dealt along a Hilbert curve; the pixel interleave and a block
+// lattice on request: rt_rank_tiles), and ONE
 // ncclGather (rccl.h:745) of the packed per-rank framebuffers to the root over xGMI.
 // Replaces the reference's single-process pixel loop (main.cpp:299-332) for
 // config 5 (final() 1000x1000x1000 over 8 GPUs); the RNG is keyed by (pixel,
@@ -41,6 +42,7 @@ struct rt_dist {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1, device = 0;
     bool aborted = false;   // ncclCommAbort after a local failure (rt_dist_render)
+    int layout = RT_LAYOUT_BLOCKS;   // how rt_dist_render splits the pixels (rt_dist_set_layout)
 };
 
 extern "C" {
@@ -120,6 +122,82 @@ int64_t rt_rank_pixels(int nx, int ny, int rank, int world, int32_t *tiles, int6
     return n;
 }
 
+// Position of cell (x, y) on the Hilbert curve over an n x n grid (n a power of 2); the
+// quadrant rotation reflects within the current sub-square (s - 1 - x), as rtnw.py's
+// restatement in tests/test_layouts.py does, so both deal the same blocks.
+static int64_t hilbert_index(int64_t n, int64_t x, int64_t y) {
+    int64_t d = 0;
+    for (int64_t s = n / 2; s > 0; s /= 2) {
+        const int64_t rx = (x & s) > 0, ry = (y & s) > 0;
+        d += s * s * ((3 * rx) ^ ry);
+        if (!ry) {
+            if (rx) {
+                x = s - 1 - x;
+                y = s - 1 - y;
+            }
+            std::swap(x, y);
+        }
+    }
+    return d;
+}
+
+// One block's pixels as 1x1 tiles, column by column (any 64 consecutive items of a full
+// 8 x 8 block are that block: one wave's claim, the 1-GPU render's coherence)
+static void emit_block(int nx, int ny, int x0, int y0, int block, int32_t *tiles, int64_t &k) {
+    for (int x = x0; x < std::min(x0 + block, nx); ++x)
+        for (int y = y0; y < std::min(y0 + block, ny); ++y) {
+            if (tiles) {
+                tiles[4 * k + 0] = x;
+                tiles[4 * k + 1] = y;
+                tiles[4 * k + 2] = 1;
+                tiles[4 * k + 3] = 1;
+            }
+            ++k;
+        }
+}
+
+int64_t rt_rank_tiles(int nx, int ny, int rank, int world, int layout, int block, int32_t *tiles, int64_t cap) {
+    if (nx <= 0 || ny <= 0 || world < 1 || rank < 0 || rank >= world || nx > 65535 || ny > 65535)
+        return fail(RT_ERR_INVALID, "rt_rank_tiles: bad argument");
+    if (layout == RT_LAYOUT_INTERLEAVED) return rt_rank_pixels(nx, ny, rank, world, tiles, cap);
+    if (layout != RT_LAYOUT_BLOCKS && layout != RT_LAYOUT_LATTICE) return fail(RT_ERR_INVALID, "rt_rank_tiles: unknown layout");
+    if (block <= 0) block = RT_LAYOUT_BLOCK;
+    const int bx = (nx + block - 1) / block, by = (ny + block - 1) / block;
+    // this rank's blocks, in claim order
+    std::vector<int64_t> mine;
+    if (layout == RT_LAYOUT_BLOCKS) {
+        // every block's Hilbert position; block k of the curve goes to rank k mod world
+        int64_t n = 1;
+        while (n < std::max(bx, by)) n *= 2;
+        std::vector<std::pair<int64_t, int64_t>> order((size_t)bx * by);
+        for (int yb = 0; yb < by; ++yb)
+            for (int xb = 0; xb < bx; ++xb) order[(size_t)yb * bx + xb] = {hilbert_index(n, xb, yb), (int64_t)yb * bx + xb};
+        std::sort(order.begin(), order.end());   // positions are distinct: the order is the curve's
+        for (size_t k = (size_t)rank; k < order.size(); k += (size_t)world) mine.push_back(order[k].second);
+    } else {
+        // the a x b interleave lattice at block granularity, row-major block order
+        int a = 1, b = 1;
+        rt_interleave_factors(world, &a, &b);
+        const int ry = rank / a, rx = rank % a;
+        for (int yb = ry; yb < by; yb += b)
+            for (int xb = rx; xb < bx; xb += a) mine.push_back((int64_t)yb * bx + xb);
+    }
+    int64_t n = 0;
+    for (const int64_t c : mine) emit_block(nx, ny, (int)(c % bx) * block, (int)(c / bx) * block, block, nullptr, n);
+    if (!tiles) return n;
+    if (cap < n) return fail(RT_ERR_INVALID, "rt_rank_tiles: buffer too small");
+    int64_t k = 0;
+    for (const int64_t c : mine) emit_block(nx, ny, (int)(c % bx) * block, (int)(c / bx) * block, block, tiles, k);
+    return n;
+}
+
+int rt_dist_set_layout(rt_dist *d, int layout) {
+    if (!d || (layout != RT_LAYOUT_BLOCKS && layout != RT_LAYOUT_INTERLEAVED && layout != RT_LAYOUT_LATTICE))
+        return fail(RT_ERR_INVALID, "rt_dist_set_layout: bad argument");
+    d->layout = layout;
+    return RT_OK;
+}
+
 int rt_unpack_tiles(const float *packed, const int32_t *tiles, int64_t ntiles, int nx, int ny, float *image) {
     if ((!packed || !tiles || !image) && ntiles) return fail(RT_ERR_INVALID, "rt_unpack_tiles: null argument");
     int64_t off = 0;
@@ -152,12 +230,12 @@ int rt_dist_render(rt_dist *d, rt_scene *s, const rt_camera_desc *cam, const rt_
     // every rank's pixel count, so that the gather's per-rank count (the largest) is agreed
     int64_t nmax = 0;
     for (int r = 0; r < d->world; ++r) {
-        const int64_t n = rt_rank_pixels(p->nx, p->ny, r, d->world, nullptr, 0);
+        const int64_t n = rt_rank_tiles(p->nx, p->ny, r, d->world, d->layout, RT_LAYOUT_BLOCK, nullptr, 0);
         if (n < 0) return (int)n;
         nmax = std::max(nmax, n);
     }
-    std::vector<int32_t> mine((size_t)rt_rank_pixels(p->nx, p->ny, d->rank, d->world, nullptr, 0) * 4);
-    rt_rank_pixels(p->nx, p->ny, d->rank, d->world, mine.data(), (int64_t)mine.size() / 4);
+    std::vector<int32_t> mine((size_t)rt_rank_tiles(p->nx, p->ny, d->rank, d->world, d->layout, RT_LAYOUT_BLOCK, nullptr, 0) * 4);
+    rt_rank_tiles(p->nx, p->ny, d->rank, d->world, d->layout, RT_LAYOUT_BLOCK, mine.data(), (int64_t)mine.size() / 4);
     const uint64_t count = (uint64_t)nmax * 3;
     float *send = nullptr, *recv = nullptr;
     hipStream_t stream = nullptr;
@@ -199,9 +277,9 @@ int rt_dist_render(rt_dist *d, rt_scene *s, const rt_camera_desc *cam, const rt_
         std::vector<float> host(count * d->world);
         if (hip_ok(hipMemcpy(host.data(), recv, host.size() * sizeof(float), hipMemcpyDeviceToHost), "hipMemcpy")) {
             for (int r = 0; r < d->world && rc == RT_OK; ++r) {
-                const int64_t n = rt_rank_pixels(p->nx, p->ny, r, d->world, nullptr, 0);
+                const int64_t n = rt_rank_tiles(p->nx, p->ny, r, d->world, d->layout, RT_LAYOUT_BLOCK, nullptr, 0);
                 std::vector<int32_t> t((size_t)n * 4);
-                rt_rank_pixels(p->nx, p->ny, r, d->world, t.data(), n);
+                rt_rank_tiles(p->nx, p->ny, r, d->world, d->layout, RT_LAYOUT_BLOCK, t.data(), n);
                 rc = rt_unpack_tiles(host.data() + (size_t)r * count, t.data(), n, p->nx, p->ny, image);
             }
         }

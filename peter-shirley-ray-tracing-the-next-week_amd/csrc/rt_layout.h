@@ -117,9 +117,6 @@ struct rt_dgroup {
 // carries (float)(1.0/(double)ref_idx), schlick r0^2 and ref_idx^2 in albedo (capi.cpp).
 // flags: 1 a texture of the material reads (u, v); 2 its texture is a constant whose
 // color is in albedo (textured kinds only: capi.cpp)
-#ifndef RT_MAT_CONST_TEX
-#define RT_MAT_CONST_TEX 1
-#endif
 struct rt_dmaterial {
     int32_t kind, texture;
     float fuzz, ref_idx;

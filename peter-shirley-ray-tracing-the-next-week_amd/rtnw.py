@@ -152,6 +152,9 @@ def lib():
             "rt_interleave_factors": (None, [ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int)]),
             "rt_rank_pixels": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                                 ctypes.c_int64]),
+            "rt_rank_tiles": (ctypes.c_int64, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_void_p, ctypes.c_int64]),
+            "rt_dist_set_layout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
             "rt_unpack_tiles": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_void_p]),
             "rt_dist_render": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, P(RtCameraDesc), P(RtRenderParams),
@@ -364,6 +367,10 @@ class Dist:
         _check(lib().rt_dist_gather(self.handle, ctypes.c_void_p(send_dev), count, ctypes.c_void_p(recv_dev), root,
                                     ctypes.c_void_p(stream)))
 
+    def set_layout(self, layout: int):
+        """rt_dist_set_layout: the split rt_dist_render uses (RT_LAYOUT_*; blocks by default)."""
+        _check(lib().rt_dist_set_layout(self.handle, layout))
+
     def render(self, scene: "Scene", cam: "Camera", params: RtRenderParams):
         """rt_dist_render: this rank's pixels -> render -> gather; the image on rank 0."""
         img = np.zeros((params.ny, params.nx, 3), np.float32) if self.rank == 0 else None
@@ -384,6 +391,20 @@ def rank_pixels_c(nx, ny, rank, world):
     _check(0 if n >= 0 else int(n))
     t = np.zeros((n, 4), np.int32)
     _check(0 if lib().rt_rank_pixels(nx, ny, rank, world, t.ctypes.data, n) == n else -1)
+    return t
+
+
+# include/rt_hip.h RT_LAYOUT_*: how a job's pixels are split over the ranks
+RT_LAYOUT_BLOCKS, RT_LAYOUT_INTERLEAVED, RT_LAYOUT_LATTICE = 0, 1, 2
+RT_LAYOUT_BLOCK = 8
+
+
+def rank_tiles_c(nx, ny, rank, world, layout, block=RT_LAYOUT_BLOCK):
+    """The C ABI's rank share (rt_rank_tiles) as 1x1 tiles in claim order."""
+    n = lib().rt_rank_tiles(nx, ny, rank, world, layout, block, None, 0)
+    _check(0 if n >= 0 else int(n))
+    t = np.zeros((n, 4), np.int32)
+    _check(0 if lib().rt_rank_tiles(nx, ny, rank, world, layout, block, t.ctypes.data, n) == n else -1)
     return t
 
 
@@ -486,85 +507,31 @@ def pixels_for_rank(nx, ny, rank, world, block=8):
     return t
 
 
-def hilbert_index(n, x, y):
-    """Position of cell (x, y) on the Hilbert curve over an n x n grid (n a power of 2)."""
-    x = np.asarray(x, dtype=np.int64).copy()
-    y = np.asarray(y, dtype=np.int64).copy()
-    d = np.zeros_like(x)
-    s = n // 2
-    while s > 0:
-        rx = (x & s) > 0
-        ry = (y & s) > 0
-        d += s * s * ((3 * rx) ^ ry)
-        # rotate the quadrant
-        flip = ~ry
-        sw = flip & rx
-        x = np.where(sw, s - 1 - x, x)
-        y = np.where(sw, s - 1 - y, y)
-        x, y = np.where(flip, y, x), np.where(flip, x, y)
-        s //= 2
-    return d
+def blocks_for_rank(nx, ny, rank, world, block=RT_LAYOUT_BLOCK):
+    """Block deal (the C ABI's rt_rank_tiles, RT_LAYOUT_BLOCKS — what rt_dist_render and
+    bench.py split a job by): the image's block x block pixel blocks, in Hilbert-curve
+    order, dealt to the ranks in turn (block k to rank k mod world) — every rank's blocks
+    spread evenly over the view (equal counts +-1), and each block keeps the 1-GPU
+    render's ray coherence: a wave's 64 items are one 8 x 8 block (pixels_for_rank's
+    lattice spreads them over a x 8 by b x 8 pixels).  Returned as 1x1 tiles, block by
+    block, each block column by column."""
+    return rank_tiles_c(nx, ny, rank, world, RT_LAYOUT_BLOCKS, block)
 
 
-def blocks_for_rank(nx, ny, rank, world, block=8):
-    """Block deal: the image's block x block pixel blocks, in Hilbert-curve order, dealt to
-    the ranks in turn (block k to rank k mod world) — every rank's blocks spread evenly
-    over the view (equal counts +-1), and each block keeps the 1-GPU render's ray
-    coherence: a wave's 64 items are one 8 x 8 block (pixels_for_rank's lattice spreads
-    them over a x 8 by b x 8 pixels).  Returned as 1x1 tiles, block by block, each block
-    column by column."""
-    bx, by = (nx + block - 1) // block, (ny + block - 1) // block
-    n = 1
-    while n < max(bx, by):
-        n *= 2
-    X, Y = np.meshgrid(np.arange(bx), np.arange(by), indexing="xy")
-    d = hilbert_index(n, X.ravel(), Y.ravel())
-    order = np.argsort(d, kind="stable")
-    mine = order[rank::world]
-    out = []
-    for k in mine:
-        x0, y0 = int(X.ravel()[k]) * block, int(Y.ravel()[k]) * block
-        xs = np.arange(x0, min(x0 + block, nx))
-        ys = np.arange(y0, min(y0 + block, ny))
-        I, J = np.meshgrid(xs, ys, indexing="ij")   # column by column
-        out.append(np.stack([I.ravel(), J.ravel()], axis=1))
-    if not out:
-        return np.zeros((0, 4), np.int32)
-    xy = np.concatenate(out)
-    t = np.ones((xy.shape[0], 4), np.int32)
-    t[:, :2] = xy
-    return t
-
-
-def lattice_blocks_for_rank(nx, ny, rank, world, block=8):
-    """Block lattice: with world = a x b, rank (ry, rx) = divmod(rank, a) renders the
-    block x block pixel blocks (bx, by) with bx = rx (mod a), by = ry (mod b) — the pixel
-    interleave's regular sub-sampling of the view at block granularity, so each wave's
-    64 items stay one 8 x 8 block (the 1-GPU render's ray coherence).  Returned as 1x1
-    tiles, block by block in row-major block order, each block column by column."""
-    a, b = interleave_factors(world)
-    ry, rx = divmod(rank, a)
-    bx, by = (nx + block - 1) // block, (ny + block - 1) // block
-    out = []
-    for yb in range(ry, by, b):
-        for xb in range(rx, bx, a):
-            x0, y0 = xb * block, yb * block
-            xs = np.arange(x0, min(x0 + block, nx))
-            ys = np.arange(y0, min(y0 + block, ny))
-            I, J = np.meshgrid(xs, ys, indexing="ij")   # column by column
-            out.append(np.stack([I.ravel(), J.ravel()], axis=1))
-    if not out:
-        return np.zeros((0, 4), np.int32)
-    xy = np.concatenate(out)
-    t = np.ones((xy.shape[0], 4), np.int32)
-    t[:, :2] = xy
-    return t
+def lattice_blocks_for_rank(nx, ny, rank, world, block=RT_LAYOUT_BLOCK):
+    """Block lattice (rt_rank_tiles, RT_LAYOUT_LATTICE): with world = a x b, rank
+    (ry, rx) = divmod(rank, a) renders the block x block pixel blocks (bx, by) with
+    bx = rx (mod a), by = ry (mod b) — the pixel interleave's regular sub-sampling of the
+    view at block granularity, so each wave's 64 items stay one 8 x 8 block.  Returned as
+    1x1 tiles, block by block in row-major block order, each block column by column."""
+    return rank_tiles_c(nx, ny, rank, world, RT_LAYOUT_LATTICE, block)
 
 
 def rank_layout(nx, ny, tile, world, order="diagonal"):
     """Tiles and packed float counts of every rank."""
-    if order == "interleaved":
-        tiles = [pixels_for_rank(nx, ny, r, world) for r in range(world)]
+    if order in ("interleaved", "blocks", "lattice"):   # 1x1 tiles (blocks, lattice: rt_rank_tiles)
+        fn = {"blocks": blocks_for_rank, "lattice": lattice_blocks_for_rank}.get(order, pixels_for_rank)
+        tiles = [fn(nx, ny, r, world) for r in range(world)]
         return tiles, [len(t) * 3 for t in tiles]
     tiles = [tiles_for_rank(nx, ny, tile, r, world, order) for r in range(world)]
     counts = [sum(w * h for _, _, w, h in t) * 3 for t in tiles]

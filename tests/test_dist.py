@@ -1,5 +1,6 @@
-"""Multi-rank path on CPU (gloo, world size 2): rank sharding (the pixel interleave
-bench.py uses, and diagonal tiles), packed
+"""Multi-rank path on CPU (gloo, world size 2): rank sharding (the Hilbert block deal
+bench.py and rt_dist_render use, the pixel interleave, the block lattice and diagonal
+tiles), packed
 per-rank buffers padded to a common length, one collective gather to rank 0,
 unpack on the root.  The per-tile renderer here is the oracle's statement of the
 kernel (the same per-pixel values the GPU produces; tests/test_gpu_parity.py
@@ -31,7 +32,7 @@ def _free_port():
 def render_rank(rank, world, order):
     tiles, counts = rtnw.rank_layout(NX, NY, TILE, world, order)
     buf = np.zeros(max(counts), np.float32)
-    if order == "interleaved":   # 1x1 tiles: this rank's pixels of the (order-independent) image
+    if order in ("interleaved", "blocks", "lattice"):   # 1x1 tiles: this rank's pixels of the image
         full, _ = O.render(O.kernel_spec("final", NX, NY, NS, seed=SEED))
         t = tiles[rank]
         buf[: 3 * len(t)] = full[t[:, 1], t[:, 0]].reshape(-1)
@@ -60,7 +61,7 @@ def _worker(rank, world, port, order, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,order", [(2, "interleaved"), (2, "diagonal")])
+@pytest.mark.parametrize("world,order", [(2, "blocks"), (2, "interleaved"), (2, "lattice"), (2, "diagonal")])
 def test_gloo_gather_equals_single_rank_image(world, order):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -76,7 +77,7 @@ def test_gloo_gather_equals_single_rank_image(world, order):
     assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
 
 
-@pytest.mark.parametrize("order", ["interleaved", "diagonal", "hashed"])
+@pytest.mark.parametrize("order", ["blocks", "interleaved", "diagonal", "hashed"])
 def test_layout_covers_image_once_and_balances_ranks(order):
     import bench
     for world in (2, 3, 4, 8):
@@ -103,14 +104,14 @@ def test_interleave_claims_are_local():
         assert np.mean(local) > 0.9, (world, np.mean(local))
 
 
-def _gpu_worker(rank, world, port, q):
-    """One rank of the product path: its interleaved pixels through librt_hip.so
-    (rt_render_tiles into device memory), gathered with gloo to rank 0."""
+def _gpu_worker(rank, world, port, q, layout=1):
+    """One rank of the product path: its pixels (rt_rank_tiles' layout) through
+    librt_hip.so (rt_render_tiles into device memory), gathered with gloo to rank 0."""
     import ctypes
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    tiles = rtnw.pixels_for_rank(NX, NY, rank, world)
-    nmax = max(len(rtnw.pixels_for_rank(NX, NY, r, world)) for r in range(world)) * 3
+    tiles = rtnw.rank_tiles_c(NX, NY, rank, world, layout)
+    nmax = max(len(rtnw.rank_tiles_c(NX, NY, r, world, layout)) for r in range(world)) * 3
     sc = rtnw.Scene.builtin("final", device=0)
     cam = rtnw.Camera.preset("cornell", NX, NY)
     p = rtnw.RenderParams(NX, NY, NS, seed=SEED)
@@ -127,7 +128,7 @@ def _gpu_worker(rank, world, port, q):
     if rank == 0:
         img = np.zeros((NY, NX, 3), np.float32)
         for r in range(world):
-            tr = rtnw.pixels_for_rank(NX, NY, r, world)
+            tr = rtnw.rank_tiles_c(NX, NY, r, world, layout)
             rtnw.unpack_tiles(gl[r][: 3 * len(tr)].numpy(), tr, img)
         q.put((img, st["samples"]))
     dist.barrier()
@@ -136,20 +137,22 @@ def _gpu_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_gloo_gather_of_product_renders_equals_single_gpu_image():
-    """World size 2 on one GPU, each rank driving librt_hip.so (not the oracle): the
+@pytest.mark.parametrize("layout", [rtnw.RT_LAYOUT_BLOCKS, rtnw.RT_LAYOUT_INTERLEAVED])
+def test_gloo_gather_of_product_renders_equals_single_gpu_image(layout):
+    """World size 2 on one GPU, each rank driving librt_hip.so (not the oracle) with the
+    C ABI's split (rt_rank_tiles: the Hilbert block deal, the pixel interleave): the
     gathered image == the 1-rank GPU image bitwise == the oracle within the bar."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q, layout)) for r in range(2)]
     for p in procs:
         p.start()
     img, samples = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert samples == len(rtnw.pixels_for_rank(NX, NY, 0, 2)) * NS
+    assert samples == len(rtnw.rank_tiles_c(NX, NY, 0, 2, layout)) * NS
     sc = rtnw.Scene.builtin("final", device=0)
     one = sc.render_tile(rtnw.Camera.preset("cornell", NX, NY), rtnw.RenderParams(NX, NY, NS, seed=SEED), 0, 0, NX, NY)
     assert np.array_equal(img.view(np.uint32), one.view(np.uint32))
@@ -168,10 +171,12 @@ def test_rccl_one_rank_communicator_gather_equals_render_tile():
     cam = rtnw.Camera.preset("cornell", nx, ny)
     p = rtnw.RenderParams(nx, ny, ns, seed=3)
     d = rtnw.Dist(rtnw.dist_unique_id(), 0, 1, 0)
-    img, st = d.render(sc, cam, p)
-    assert st["samples"] == nx * ny * ns
     ref = sc.render_tile(cam, p, 0, 0, nx, ny)
-    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    for layout in (rtnw.RT_LAYOUT_BLOCKS, rtnw.RT_LAYOUT_INTERLEAVED, rtnw.RT_LAYOUT_LATTICE):
+        d.set_layout(layout)
+        img, st = d.render(sc, cam, p)
+        assert st["samples"] == nx * ny * ns
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
     data = torch.arange(1000, dtype=torch.float32, device="cuda")
     recv = torch.zeros(1000, dtype=torch.float32, device="cuda")
     d.gather(data.data_ptr(), 1000, recv.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)

@@ -314,13 +314,6 @@ def test_block_deal_partitions_the_image():
                 assert (blk == blk[:, :1]).all()
         assert (seen == 1).all()
         assert max(counts) - min(counts) <= 64
-    # consecutive Hilbert indices are neighbouring cells
-    n = 16
-    X, Y = np.meshgrid(np.arange(n), np.arange(n), indexing="xy")
-    d = rtnw.hilbert_index(n, X.ravel(), Y.ravel())
-    o = np.argsort(d)
-    assert np.array_equal(np.sort(d), np.arange(n * n))
-    assert (np.abs(np.diff(X.ravel()[o])) + np.abs(np.diff(Y.ravel()[o])) == 1).all()
 
 
 def test_math_probe_rejects_bad_arguments():

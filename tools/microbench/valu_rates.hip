@@ -58,6 +58,15 @@ K32D(k_min3_f32_d, ASM)
 #define ASM "v_med3_f32 %0, %0, %1, %2"
 K32D(k_med3_f32_d, ASM)
 #undef ASM
+#define ASM "v_fma_mix_f32 %0, %2, %1, %0 op_sel_hi:[1,0,0]"
+K32D(k_fma_mix_lo_d, ASM)
+#undef ASM
+#define ASM "v_fma_mix_f32 %0, %2, %1, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+K32D(k_fma_mix_hi_d, ASM)
+#undef ASM
+#define ASM "v_cvt_f32_f16 %0, %1"
+K32D(k_cvt_f32_f16_d, ASM)
+#undef ASM
 #define ASM "v_add3_u32 %0, %0, %1, %2"
 K32D(k_add3_u32_d, ASM)
 #undef ASM
@@ -292,7 +301,9 @@ int main() {
         {"v_max_f32_e64", k_max_f32_e64}, {"v_mul_f32_e64", k_mul_f32_e64}, {"v_add3_u32", k_add3_u32},
         {"v_fma_f32 (distinct)", k_fma_f32_d}, {"v_min3_f32 (distinct)", k_min3_f32_d},
         {"v_med3_f32 (distinct)", k_med3_f32_d}, {"v_add3_u32 (distinct)", k_add3_u32_d},
-        {"v_cndmask_b32 (sgpr mask, distinct)", k_cndmask_s_d}, {"v_mad_u32_u24 (distinct)", k_mad_u32_u24_d}};
+        {"v_cndmask_b32 (sgpr mask, distinct)", k_cndmask_s_d}, {"v_mad_u32_u24 (distinct)", k_mad_u32_u24_d},
+        {"v_fma_mix_f32 lo (distinct)", k_fma_mix_lo_d}, {"v_fma_mix_f32 hi (distinct)", k_fma_mix_hi_d},
+        {"v_cvt_f32_f16 (distinct)", k_cvt_f32_f16_d}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
