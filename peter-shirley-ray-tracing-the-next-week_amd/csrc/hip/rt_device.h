@@ -502,6 +502,7 @@ struct Counters {
     // material divergence of the shading stage: wave passes through the scatter
     // branches, the distinct materials each pass ran, and the lanes that scattered
     uint64_t w_shade = 0, w_kinds = 0, l_scatter = 0;
+    uint64_t ball[RT_BALL_N] = {0, 0, 0, 0, 0, 0, 0, 0};   // the ball waves (rt_layout.h RT_BALL_*), wave-level
     __device__ __forceinline__ void prim(int kind) {
         const int k = kind & 0xff;
         if (k == RT_PRIM_SPHERE) spheres++;

@@ -48,6 +48,11 @@ struct RtKernelArgs {
     int scan;               // 1: flat scan of the groups instead of a BVH (small scenes, rt_layout.h)
     uint32_t nprims;        // surface primitives (flat scan: all copied to LDS)
     int nprescan;           // BVH modes: primitives [0, nprescan) are outside the BVH, tested first in lockstep
+    int cell_first, cell_n;   // BVH modes: the medium cell's primitive copies [cell_first, cell_first + cell_n) ...
+    float cell_c[3], cell_r2; //     ... and its ball (centre, squared radius): capi.cpp rt_scene_create
+    int ball_waves;           // waves per workgroup that take the medium cell's paths first (LDS media variant) ...
+    int ball_batch;           //     ... their ready batch (the others': RT_READY_BATCH) ...
+    int ball_claim;           //     ... and the busy lanes below which they claim new samples
     int lds_nodes;          // 1: BVH2 nodes copied to LDS (RT_LDS_BLOCK workgroups, one per CU)
     int stack_depth;        // traversal stack entries per lane of the LDS variant (BVH depth + 1)
     // camera (camera.h members)

@@ -64,6 +64,16 @@ namespace {
 // Pre-made sample starts per wave (refill): one per lane.
 #define RT_PRE 64
 
+// Path pools of the ball waves (stage 6): paths whose segment starts inside the medium
+// cell's ball, and paths that left it, waiting in LDS for a wave of their kind (80 B each)
+#ifndef RT_BALL_POOL
+#define RT_BALL_POOL 28
+#endif
+#ifndef RT_NORM_POOL
+#define RT_NORM_POOL 24
+#endif
+typedef unsigned U4p __attribute__((ext_vector_type(4)));
+
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -105,6 +115,13 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                    kChecker = (kFeat & RT_FEAT_CHECKER) != 0, kPrescan = (kFeat & RT_FEAT_PRESCAN) != 0,
                    kMedia = (kFeat & RT_FEAT_MEDIA) != 0;
     constexpr bool kLds = kMode == 1, kScan = kMode == 2;
+    // the ball waves (stage 6) and the medium cell that ends their paths' closest-hit searches
+    // (stage 3): the media variant without instance chains (final(); a cell needs a medium
+    // bounded by one plain sphere, and the instance variants have no registers to spare) with
+    // the BVH2 in LDS.  The cell is tested in ball waves only: in the others, whose lanes
+    // mostly start outside the ball, its lockstep tests cost every lane (c4 +3.8 %)
+    constexpr bool kBall = kMedia && !kInst && kFeat != RT_FEAT_ALL && kLds && kWidth == 2;
+    constexpr bool kCell = kBall;
     // the LDS node layout (rt_device.h RtSplit): dword planes in the media variants (final()),
     // float4 planes otherwise, as each measured fastest
     constexpr int kSplit = rt_lds_split(kMode, kFeat, kWidth);
@@ -119,6 +136,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
     __shared__ uint2 lds_pre_cp[kBlock / 64][RT_PRE];   // each entry's (sample chunk, job pixel)
+    // stage 6's path pools (kBall): [0] paths inside the ball, [1] paths outside; a lock and
+    // the two counts
+    __shared__ U4p lds_pool_in[kBall ? RT_BALL_POOL : 1][5];
+    __shared__ U4p lds_pool_out[kBall ? RT_NORM_POOL : 1][5];
+    __shared__ uint32_t lds_pool_ctl[4];
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
@@ -133,6 +155,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // the media records are read from LDS (one broadcast read per medium)
     if (kMedia) load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) {
+        lds_pool_ctl[0] = lds_pool_ctl[1] = lds_pool_ctl[2] = lds_pool_ctl[3] = 0;
         store_camera(A, lds_cam);
         lds_mconst = LogConsts{1.0 / 7, -1.0 / 6, 0.2, -0.25, 1.0 / 3};
     }
@@ -214,8 +237,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     };
     // a new ray segment: closest-hit search from the root (hitable_list.h:20-32)
     bool fresh = false;   // a new segment the pre-scan has not seen yet
-    auto begin_segment = [&]() {
-        if (kPrescan) fresh = true;
+    auto begin_segment = [&](bool counted = true) {
+        if (kPrescan || kCell) fresh = true;
         // LDS mode: byte offsets (the root is interior there)
         node = kLds ? lds_node_ref<kSplit>(A.root) : A.root;
         sp = 0;
@@ -223,7 +246,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         best_key = 0x7FFFFFFF;
         best_prim = 0xFFFFFFFFu;
         phase = A.has_bvh ? PH_TRAV : PH_READY;
-        if (kCount) cnt.segments++;
+        if (kCount && counted) cnt.segments++;
     };
 
     // Sample starts are made for 64 work items at once, by all lanes of the wave
@@ -285,17 +308,124 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         pre_count = n;
         pool_next += n;
     };
+    // ---- stage 6's path pools (kBall; DESIGN.md §5c "ball waves") ----------------------
+    // The workgroup's last A.ball_waves waves gather the paths whose segment starts inside
+    // the medium cell's ball: their closest-hit searches end at the cell's few primitives
+    // with no BVH descent, so a wave made of them skips the traversal stage.  Paths move
+    // between waves through two LDS pools at segment starts (the whole path state, 80 B:
+    // ray, throughput, depth, both drand48 states, the work item and its partial sum), so
+    // every sample's draws, adds and slab slot are its own wherever it runs: images are
+    // bitwise unchanged.  One spin lock guards both pools; a wave leaves the kernel only
+    // after seeing both pools empty, so no path is stranded.
+    const bool ballrole = kBall && (int)wave >= kBlock / 64 - A.ball_waves;   // wave-uniform
+    typedef __attribute__((address_space(3))) volatile uint32_t LdsVU;
+    auto pool_peek = [&](int k) -> uint32_t {   // a racy hint; decisions are made under the lock
+        return __builtin_amdgcn_readfirstlane(((LdsVU *)lds_pool_ctl)[1 + k]);
+    };
+    auto pool_lock = [&]() {
+        if (lane == 0)
+            while (atomicCAS(&lds_pool_ctl[0], 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    };
+    auto pool_unlock = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) atomicExch(&lds_pool_ctl[0], 0u);
+    };
+    auto pool_entry = [&](int k, uint32_t e) -> U4p * { return k == 0 ? lds_pool_in[e] : lds_pool_out[e]; };
+    // lanes with `want` (a fresh segment) leave for pool k while it has room; returns who left
+    auto pool_push = [&](int k, bool want) -> bool {
+        const uint64_t M = wballot(want);
+        if (M == 0ull) return false;
+        const uint32_t cap = k == 0 ? RT_BALL_POOL : RT_NORM_POOL;
+        if (pool_peek(k) >= cap) return false;
+        pool_lock();
+        const uint32_t n = __builtin_amdgcn_readfirstlane(((LdsVU *)lds_pool_ctl)[1 + k]);
+        const uint32_t take = min((uint32_t)__popcll(M), cap - min(n, cap));
+        const uint32_t rank = lanes_below(M);
+        const bool go = want && rank < take;
+        if (go) {
+            U4p *E = pool_entry(k, n + rank);
+            E[0] = U4p{__float_as_uint(r.o.x), __float_as_uint(r.o.y), __float_as_uint(r.o.z), __float_as_uint(r.time)};
+            E[1] = U4p{__float_as_uint(r.d.x), __float_as_uint(r.d.y), __float_as_uint(r.d.z), __float_as_uint(beta.x)};
+            E[2] = U4p{__float_as_uint(beta.y), __float_as_uint(beta.z), __float_as_uint(part.x), __float_as_uint(part.y)};
+            E[3] = U4p{__float_as_uint(part.z), item, (uint32_t)s_cur, (uint32_t)s_end};
+            E[4] = U4p{(uint32_t)g.x, (uint32_t)(g.x >> 32) | ((uint32_t)depth << 16), (uint32_t)g.xm, (uint32_t)(g.xm >> 32)};
+        }
+        if (lane == 0) ((LdsVU *)lds_pool_ctl)[1 + k] = n + take;
+        pool_unlock();
+        if (kCount && lane == 0) cnt.ball[k == 0 ? RT_BALL_PUSH_IN : RT_BALL_PUSH_OUT] += take;
+        return go;
+    };
+    // lanes with `need` take paths from pool k (a fresh segment each); returns who took one
+    auto pool_take = [&](int k, bool need) -> bool {
+        const uint64_t M = wballot(need);
+        if (M == 0ull || pool_peek(k) == 0u) return false;
+        pool_lock();
+        const uint32_t n = __builtin_amdgcn_readfirstlane(((LdsVU *)lds_pool_ctl)[1 + k]);
+        const uint32_t take = min((uint32_t)__popcll(M), n);
+        const uint32_t rank = lanes_below(M);
+        const bool got = need && rank < take;
+        if (got) {
+            const U4p *E = pool_entry(k, n - take + rank);
+            const U4p e0 = E[0], e1 = E[1], e2 = E[2], e3 = E[3], e4 = E[4];
+            r.o = mk(__uint_as_float(e0.x), __uint_as_float(e0.y), __uint_as_float(e0.z));
+            r.time = __uint_as_float(e0.w);
+            r.d = mk(__uint_as_float(e1.x), __uint_as_float(e1.y), __uint_as_float(e1.z));
+            beta = mk(__uint_as_float(e1.w), __uint_as_float(e2.x), __uint_as_float(e2.y));
+            part = mk(__uint_as_float(e2.z), __uint_as_float(e2.w), __uint_as_float(e3.x));
+            item = e3.y;
+            s_cur = (int)e3.z;
+            s_end = (int)e3.w;
+            g.x = ((uint64_t)(e4.y & 0xFFFFu) << 32) | e4.x;
+            depth = (int)(e4.y >> 16);
+            g.xm = ((uint64_t)e4.w << 32) | e4.z;
+        }
+        if (lane == 0) ((LdsVU *)lds_pool_ctl)[1 + k] = n - take;
+        pool_unlock();
+        if (kCount && lane == 0) cnt.ball[RT_BALL_TAKEN] += take;
+        if (got) {
+            finished = false;
+            pre_have = false;
+            begin_segment(false);   // (the segment was counted where it began)
+        }
+        return got;
+    };
+
     // retire a finished work item (its sum to the slab), hand the lanes without work
-    // the next pre-made sample starts (one global atomic per A.claim items)
-    auto retire_and_claim = [&]() {
+    // the next pre-made sample starts (one global atomic per A.claim items).  top: the call
+    // at the top of the iteration, the only one that takes pooled paths (kBall; one inlined
+    // copy of the path-state load, where two spilled); in the other, a ball wave whose pool
+    // holds paths leaves its idle lanes for the next top
+    auto retire_and_claim = [&](bool top) {
         if (phase == PH_IDLE && !finished && item != 0xFFFFFFFFu && s_cur == s_end) {
-            float *sl = A.slab + (size_t)item * RT_SLAB_FLOATS;   // 12 B per item (16 with RT_SLAB_F4)
+            float *sl = A.slab + (size_t)item * RT_SLAB_FLOATS;   // 12 B per item
             sl[0] = part.x;
             sl[1] = part.y;
             sl[2] = part.z;
             item = 0xFFFFFFFFu;
         }
         bool need = phase == PH_IDLE && !finished && item == 0xFFFFFFFFu;
+        if constexpr (kBall) {
+            if (top) {
+                // a ball wave takes the ball's paths first, the others the paths that left
+                // it; lanes that found no work before (finished) look again: the pools refill
+                need = phase == PH_IDLE && item == 0xFFFFFFFFu;
+                // pool 0 holds the ball's paths, 1 the others'; with the claims exhausted a
+                // wave whose own pool is empty takes from the other
+                const bool other = exhausted && pool_peek(ballrole ? 0 : 1) == 0u;
+                const int k = (other == ballrole) ? 1 : 0;
+                if (pool_take(k, need)) need = false;
+            }
+            if (ballrole && !exhausted) {
+                // a ball wave claims new samples only while fewer than A.ball_claim of its lanes
+                // hold a path, and outside the top only with its pool empty (its idle lanes wait
+                // for the pool's paths at the next top); lanes left idle have no item
+                const uint32_t busy = (uint32_t)__popcll(wballot(!(phase == PH_IDLE && item == 0xFFFFFFFFu)));
+                if ((!top && pool_peek(0) != 0u) || busy >= (uint32_t)A.ball_claim) return;
+            }
+        }
         uint64_t need_mask = wballot(need);
         while (need_mask != 0ull) {
             if (pre_count == 0) {
@@ -384,13 +514,15 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // (the first iteration, and paths that ended after the shading stage's
         // cooperative rounds: a metal's absorbed reflection; the others start their
         // next sample inside stage 5)
-        retire_and_claim();
+        retire_and_claim(true);
         const uint64_t live = wballot(!finished);
-        if (live == 0ull) break;
+        // (kBall) a wave leaves only with both pools empty: paths another wave left there are
+        // taken by the next iteration's retire_and_claim (this one runs with no lane active)
+        if (live == 0ull && (!kBall || (pool_peek(0) | pool_peek(1)) == 0u)) break;
         // the pool is dry and few paths are left: the launch's end waits on their latency
         const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
         {
-            const bool starting = phase == PH_IDLE && !finished;
+            const bool starting = phase == PH_IDLE && !finished && item != 0xFFFFFFFFu;
             float cu_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f, cv_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f;   // starting lanes only
             camera_begin(starting, cu_, cv_);
             const V3 disk = coop_reject<2, kCount>(starting, g, slots, jt, lane, cnt, DiskCand());
@@ -438,6 +570,34 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 if (act) phase = PH_READY;
             }
         } else {
+            // the medium cell (capi.cpp): a new segment starting inside the ball tests the
+            // primitives near it; a hit before the ray leaves the ball is the closest of
+            // all (every other primitive lies outside), and the search ends without a descent
+            if (kCell && ballrole && A.cell_n > 0) {
+                bool in = false;
+                float tsafe = 0.f;
+                if (fresh && phase == PH_TRAV) {
+                    const V3 oc = sub(r.o, mk(A.cell_c[0], A.cell_c[1], A.cell_c[2]));
+                    const float a = dot(r.d, r.d), b = dot(oc, r.d), cc = dot(oc, oc) - A.cell_r2;
+                    if (cc < 0.f && a > 0.f) {
+                        // where the ray leaves the ball: the larger root, without cancellation
+                        // (approximate square root and reciprocals, ~1 ulp each: a bound, not a result)
+                        const float q = __builtin_amdgcn_sqrtf(b * b - a * cc);
+                        const float te = b >= 0.f ? -cc * __builtin_amdgcn_rcpf(b + q) : (q - b) * __builtin_amdgcn_rcpf(a);
+                        tsafe = te * (1.f - 1.f / 4096);   // below it by far more than its rounding
+                        in = true;
+                    }
+                }
+                if (wballot(in) != 0ull) {
+                    lockstep_prims<kCount, kInst, true>((const ConstF4 *)A.prims, A.cell_first, A.cell_n, A.insts, r, A.tmin,
+                                                        in, -1, best_t, best_key, best_prim, cnt);
+                    if (in && best_t < tsafe) phase = PH_READY;
+                    if (kCount) {
+                        const uint64_t decided = wballot(in && phase == PH_READY);
+                        if (lane == 0) cnt.ball[ballrole ? RT_BALL_CELL_BALL : RT_BALL_CELL_OTHER] += (uint64_t)__popcll(decided);
+                    }
+                }
+            }
             // pre-scan: the scene's largest primitives (capi.cpp), kept out of the BVH,
             // tested in lockstep by every lane with a new segment before its descent;
             // their hits also shorten best_t, which culls more of the BVH
@@ -446,11 +606,16 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 if (wballot(fr) != 0ull)
                     lockstep_prims<kCount, kInst, true>((const ConstF4 *)A.prims, 0, A.nprescan, A.insts, r, A.tmin, fr, -1,
                                                         best_t, best_key, best_prim, cnt);
-                fresh = false;
+            }
+            if (kPrescan || kCell) fresh = false;
+            if (kCount && ballrole && lane == 0) {
+                cnt.ball[RT_BALL_ITERS]++;
+                cnt.ball[RT_BALL_LIVE] += (uint64_t)__popcll(live);
             }
             for (;;) {
                 if (wballot(phase == PH_TRAV) == 0ull) break;
-                if (__popcll(wballot(phase == PH_READY)) >= RT_READY_BATCH) break;
+                if (__popcll(wballot(phase == PH_READY)) >= (ballrole ? A.ball_batch : RT_READY_BATCH)) break;
+                if (kCount && ballrole && lane == 0) cnt.ball[RT_BALL_ROUNDS]++;
                 if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
                     Slab sl = make_slab<kSplit>(r, A.tmin);
@@ -545,8 +710,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             }
         }
         if (ends) end_path(mul(beta, shade_emitted(A, have, r, rd, st)));
-        retire_and_claim();
-        const bool starting = phase == PH_IDLE && !finished;
+        retire_and_claim(false);
+        // (a lane left without work by a ball wave's claim, waiting for the pool, has no item)
+        const bool starting = phase == PH_IDLE && !finished && item != 0xFFFFFFFFu;
         float cu_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f, cv_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f;   // starting lanes only
         camera_begin(starting, cu_, cv_);
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
@@ -571,6 +737,20 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         mark(4);
         camera_finish(starting, cu_, cv_, pt, false);
         if (seg || starting) begin_segment();
+        // ---- 6. regroup (kBall): a scattered path whose new segment starts inside the
+        // medium cell's ball leaves a normal wave for the ball waves' pool, one that starts
+        // outside leaves a ball wave for the others' pool (while the pool has room); the
+        // lane takes new work at the next claim
+        if constexpr (kBall) {
+            if (A.ball_waves > 0 && A.cell_n > 0) {
+                const V3 oc = sub(r.o, mk(A.cell_c[0], A.cell_c[1], A.cell_c[2]));
+                const bool inball = dot(oc, oc) < A.cell_r2;
+                if (pool_push(ballrole ? 1 : 0, seg && (inball != ballrole))) {
+                    phase = PH_IDLE;
+                    item = 0xFFFFFFFFu;
+                }
+            }
+        }
         mark(3);
     }
     if (kProf && lane == 0) {
@@ -609,6 +789,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
     }
 
+    if (kCount && kBall && lane == 0)
+        for (int k = 0; k < RT_BALL_N; ++k)
+            if (cnt.ball[k]) atomicAdd(&A.stats[RT_STAT_BALL + k], (unsigned long long)cnt.ball[k]);
     if (kCount) {
         uint64_t v[RT_CNT_N] = {cnt.samples, cnt.segments, cnt.nodes, cnt.spheres, cnt.mspheres, cnt.rects,
                                 cnt.instanced, cnt.media, cnt.shades, cnt.noise};

@@ -157,6 +157,9 @@ struct rt_scene {
          *insts = nullptr, *ranvec = nullptr, *perm = nullptr, *texels = nullptr, *groups = nullptr;
     bool scan = false;            // flat scan of the primitive groups instead of the BVH (small scenes)
     int nprescan = 0;             // BVH scenes: largest primitives tested in lockstep before the BVH
+    // medium cell (rt_scene_create): primitives [cell_first, cell_first + cell_n) are copies of those near the ball
+    int cell_first = 0, cell_n = 0;
+    float cell_c[3] = {0, 0, 0}, cell_r2 = 0;
     int ngroups = 0;
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
@@ -461,8 +464,55 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
                          ((g.kinds >> 24) & 0xff) + g.nyz;
         if (runs != g.count) return cleanup(fail(RT_ERR_INVALID, "flat scan: a group's kind counts do not add up"));
     }
-    std::vector<rt_dprim> prims(d->nprims), bprims(d->nboundary);
-    for (int i = 0; i < d->nprims; i++) {
+    // Medium cell (BVH modes; rt_kernel.hip stages 3 and 6): a path inside a dense medium
+    // scatters there segment after segment (final(): a third of all segments start inside
+    // the subsurface sphere), and every segment's closest-hit search starts from the BVH
+    // root.  For one medium bounded by a sphere (c, R) — the densest such — the primitives
+    // whose boxes reach within R + m of c (m = R / 64 + 1e-3 |c|) are listed (at most
+    // RT_CELL_MAX, appended to the device primitives as copies: same record, same key); a
+    // ray starting within R + m / 2 of c tests just them, and if the nearest lies before the
+    // ray leaves that ball, no other primitive (all are outside R + m) can be nearer: the
+    // search ends there with the same (t, key) winner as the full one.  The kernel's ball
+    // waves gather such paths (RtKernelArgs.ball_waves).  RTNW_CELL=0 disables it.
+    s->cell_n = 0;
+    if (!s->scan && d->nprims > 0) {
+        bool want = true;
+        if (const char *e = std::getenv("RTNW_CELL")) want = std::atoi(e) != 0;
+        double best_density = -1;
+        std::vector<int> cell;
+        for (int i = 0; want && i < d->nmedia; i++) {
+            const rt_medium &m = d->media[i];
+            if (m.boundary_count != 1) continue;
+            const rt_prim &bp = d->boundary_prims[m.boundary_first];
+            if (bp.kind != RT_PRIM_SPHERE || bp.instance >= 0 || !(m.density > best_density)) continue;
+            const double c[3] = {bp.p[0], bp.p[1], bp.p[2]}, R = std::fabs((double)bp.p[3]);
+            const double cmax = std::max(std::fabs(c[0]), std::max(std::fabs(c[1]), std::fabs(c[2])));
+            const double mg = R / 64 + 1e-3 * cmax, reach = R + mg;
+            if (!(R > 0) || !std::isfinite(reach)) continue;
+            std::vector<int> near;
+            for (int q = 0; q < d->nprims && (int)near.size() <= RT_CELL_MAX; q++) {
+                float lo[3], hi[3];
+                rtnw::prim_bounds(d->prims[q], d->instances, d->time0, d->time1, lo, hi);
+                double d2 = 0;
+                for (int k = 0; k < 3; k++) {
+                    const double v = std::max(std::max((double)lo[k] - c[k], c[k] - (double)hi[k]), 0.0);
+                    d2 += v * v;
+                }
+                if (!(d2 > reach * reach)) near.push_back(q);   // (a NaN box counts as near)
+            }
+            if (near.empty() || (int)near.size() > RT_CELL_MAX) continue;
+            best_density = m.density;
+            s->cell_n = (int)near.size();
+            for (int k = 0; k < 3; k++) s->cell_c[k] = (float)c[k];
+            const double rk = R + mg / 2;
+            s->cell_r2 = (float)(rk * rk);
+            cell = near;
+        }
+        s->cell_first = (int)order.size();
+        for (int q : cell) order.push_back(q);
+    }
+    std::vector<rt_dprim> prims(order.size()), bprims(d->nboundary);
+    for (int i = 0; i < (int)order.size(); i++) {
         const int src = order[i];
         prims[i] = to_dprim(d->prims[src], src);
         s->has_moving |= d->prims[src].kind == RT_PRIM_MOVING_SPHERE;
@@ -644,6 +694,21 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     return RT_OK;
 }
 
+// Waves per LDS workgroup that gather the medium cell's paths (rt_kernel.hip stage 6);
+// env RTNW_BALL_WAVES (0: none) for A/B runs.  Their ready batch (RTNW_BALL_BATCH) and the
+// busy lanes below which they claim new samples (RTNW_BALL_CLAIM).
+#define RT_BALL_WAVES 3
+#define RT_BALL_BATCH 48
+#define RT_BALL_CLAIM 64
+static int env_int(const char *name, int dflt, int lo, int hi) {
+    if (const char *e = std::getenv(name)) return std::max(lo, std::min(hi, std::atoi(e)));
+    return dflt;
+}
+static int ball_waves() {
+    if (const char *e = std::getenv("RTNW_BALL_WAVES")) return std::max(0, std::min(RT_LDS_BLOCK / 64, std::atoi(e)));
+    return RT_BALL_WAVES;
+}
+
 // Small claims per wave at the end of a launch (render_tiles' claim sizes).
 #define RT_TAIL_CLAIMS 32
 
@@ -817,6 +882,13 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.groups = (const float4 *)s->groups;
     a.ngroups = s->ngroups;
     a.nprescan = s->nprescan;
+    a.cell_first = s->cell_first;
+    a.cell_n = s->cell_n;
+    for (int k = 0; k < 3; k++) a.cell_c[k] = s->cell_c[k];
+    a.cell_r2 = s->cell_r2;
+    a.ball_waves = ball_waves();
+    a.ball_batch = env_int("RTNW_BALL_BATCH", RT_BALL_BATCH, 1, 64);
+    a.ball_claim = env_int("RTNW_BALL_CLAIM", RT_BALL_CLAIM, 0, 64);
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = scene_features(s);
@@ -958,6 +1030,17 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
             stats->wave_shade_passes = (double)sh[0];
             stats->wave_shade_kinds = (double)sh[1];
             stats->lane_scatters = (double)sh[2];
+            if (std::getenv("RTNW_TRACE")) {   // the ball waves (rt_kernel.hip stage 6), diagnostics only
+                unsigned long long b[RT_BALL_N];
+                HIP_TRY(hipMemcpy(b, (unsigned long long *)s->stats + RT_STAT_BALL, sizeof b, hipMemcpyDeviceToHost));
+                std::fprintf(stderr,
+                             "rtnw ball waves: iterations %llu, live lanes / iteration %.1f, traversal rounds / iteration %.2f, "
+                             "cell-decided segments in ball waves %llu, in other waves %llu (of %.0f), pushed in %llu, "
+                             "pushed out %llu, taken %llu\n",
+                             b[RT_BALL_ITERS], b[RT_BALL_ITERS] ? (double)b[RT_BALL_LIVE] / b[RT_BALL_ITERS] : 0.0,
+                             b[RT_BALL_ITERS] ? (double)b[RT_BALL_ROUNDS] / b[RT_BALL_ITERS] : 0.0, b[RT_BALL_CELL_BALL],
+                             b[RT_BALL_CELL_OTHER], stats->segments, b[RT_BALL_PUSH_IN], b[RT_BALL_PUSH_OUT], b[RT_BALL_TAKEN]);
+            }
         }
         if (prof) {
             unsigned long long c[RT_STATS_LEN];

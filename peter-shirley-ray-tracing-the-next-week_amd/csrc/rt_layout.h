@@ -107,6 +107,8 @@ struct rt_dprim {
 #define RT_SCAN_MAX 64
 // BVH scenes: at most this many of the largest primitives are pre-scanned (capi.cpp).
 #define RT_PRESCAN_MAX 8
+// The medium cell: at most this many primitives near a dense medium's ball (capi.cpp).
+#define RT_CELL_MAX 4
 struct rt_dgroup {
     int32_t first, count, instance, kinds;
     float bx[4], bz[2];
@@ -159,5 +161,11 @@ enum {
 // RT_FLAG_PROFILE: cycles in the material scatter branches).
 enum {
     RT_STAT_PROF = RT_CNT_N, RT_STAT_WAVE = RT_CNT_N + 4, RT_STAT_TIME = RT_CNT_N + 9, RT_STAT_SHADE = RT_CNT_N + 16,
-    RT_STATS_LEN = RT_CNT_N + 20
+    RT_STAT_BALL = RT_CNT_N + 20,   // RT_FLAG_COUNT, the ball waves (rt_kernel.hip stage 6): RT_BALL_*
+    RT_STATS_LEN = RT_CNT_N + 28
 };
+// ball-wave counters: ball-wave iterations, their live lanes and traversal rounds summed over
+// them, segments the medium cell decided in ball / other waves, paths pushed into the ball's
+// pool / the others' pool, paths taken from either
+enum { RT_BALL_ITERS = 0, RT_BALL_LIVE, RT_BALL_ROUNDS, RT_BALL_CELL_BALL, RT_BALL_CELL_OTHER, RT_BALL_PUSH_IN,
+       RT_BALL_PUSH_OUT, RT_BALL_TAKEN, RT_BALL_N };

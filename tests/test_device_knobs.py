@@ -29,6 +29,8 @@ KNOBS = {
     "RT_DESCEND_TAIL_DRY": ["4"],
     "RT_LDS_MEDIA": ["1", "16"],
     "RT_SHADE_LEAN": ["0", "127"],          # every lean bit off / on (2 and 8 spill: off by default)
+    "RT_BALL_POOL": ["8", "64"],            # the ball waves' path pools (rt_kernel.hip stage 6)
+    "RT_NORM_POOL": ["8", "64"],
     "RT_KNOB_CHECK": [""],                  # this test's own build mode
 }
 

@@ -540,3 +540,41 @@ def test_shade_divergence_counters(scene, one_material):
         assert kinds == passes
     else:
         assert passes < kinds <= 4 * passes
+
+
+def test_ball_waves_leave_the_image_bitwise_unchanged(monkeypatch):
+    """The ball waves (rt_kernel.hip stage 6) move paths between waves at segment starts
+    through two LDS pools and end the searches of segments starting inside final()'s dense
+    medium at the medium cell's primitives: every sample's draws, adds and slab slot stay
+    its own, so the image is the same bit for bit with no ball waves, the default, more
+    ball waves than normal ones, and every wave a ball wave; with the medium cell off too;
+    with chunks of several samples (the item's partial sum moves with the path) and over
+    several slab batches; and equal to the oracle on crops."""
+    nx, ny, ns = 160, 120, 24
+    cam = rtnw.Camera.preset("cornell", nx, ny)
+    sc = rtnw.Scene.builtin("final")
+    imgs = {}
+    for w in ("0", "3", "12", "16"):
+        for chunk in (1, 4):
+            monkeypatch.setenv("RTNW_BALL_WAVES", w)
+            p = rtnw.RenderParams(nx, ny, ns, seed=33, chunk=chunk)
+            img, st = sc.render_tile(cam, p, 0, 0, nx, ny, stats=True)
+            imgs[(w, chunk)] = img
+            if w == "3" and chunk == 1:
+                p2 = rtnw.RenderParams(nx, ny, ns, seed=33, chunk=chunk, flags=rtnw.RT_FLAG_COUNT)
+                _, cst = sc.render_tile(cam, p2, 0, 0, nx, ny, stats=True)
+                assert cst["samples"] == nx * ny * ns
+    ref = imgs[("0", 1)]
+    for (w, chunk), img in imgs.items():   # (chunks of several samples sum in another order)
+        assert np.array_equal(img.view(np.uint32), imgs[("0", chunk)].view(np.uint32)), (w, chunk)
+    monkeypatch.setenv("RTNW_BALL_WAVES", "3")
+    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(nx * ny * 12 * 5))   # 5 samples per launch: 5 batches
+    batched = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=33), 0, 0, nx, ny)
+    assert np.array_equal(batched.view(np.uint32), ref.view(np.uint32))
+    monkeypatch.delenv("RTNW_SLAB_BUDGET")
+    monkeypatch.setenv("RTNW_CELL", "0")
+    nocell = rtnw.Scene.builtin("final").render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=33), 0, 0, nx, ny)
+    assert np.array_equal(nocell.view(np.uint32), ref.view(np.uint32))
+    for (x0, y0) in ((72, 40), (0, 0), (152, 112)):   # the subsurface sphere's pixels, and corners
+        o = oracle_render("final", nx, ny, ns, seed=33, chunk=1, rect=(x0, y0, 8, 8))
+        assert_exact(pixel_exact(ref[y0:y0 + 8, x0:x0 + 8], o))
