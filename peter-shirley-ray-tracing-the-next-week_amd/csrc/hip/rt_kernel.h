@@ -49,7 +49,8 @@ struct RtKernelArgs {
     uint32_t nprims;        // surface primitives (flat scan: all copied to LDS)
     int nprescan;           // BVH modes: primitives [0, nprescan) are outside the BVH, tested first in lockstep
     int cell_first, cell_n;   // BVH modes: the medium cell's primitive copies [cell_first, cell_first + cell_n) ...
-    float cell_c[3], cell_r2; //     ... and its ball (centre, squared radius): capi.cpp rt_scene_create
+    float cell_c[3], cell_r2; //     ... and its ball (centre, squared radius): capi.cpp rt_scene_create ...
+    float cell_rin2;          //     ... and the squared radius inside which a ray counts as inside whatever its direction
     int ball_waves;           // waves per workgroup that take the medium cell's paths first (LDS media variant) ...
     int ball_batch;           //     ... their ready batch (the others': RT_READY_BATCH) ...
     int ball_claim;           //     ... and the busy lanes below which they claim new samples

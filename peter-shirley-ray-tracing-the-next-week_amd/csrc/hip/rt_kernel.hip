@@ -223,6 +223,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
 
     Counters cnt;
     uint64_t prof[5] = {0, 0, 0, 0, 0};   // claim, traverse, media, shade, of which scatter branches
+    uint64_t prof_iters = 0;              // (kProf) this wave's loop iterations
     uint64_t stamp = kProf ? __builtin_amdgcn_s_memtime() : 0;
     // wave timeline (kProf): start, first sight of the empty pool, end (s_memrealtime: one clock for all CUs)
     const uint64_t rt_start = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -743,8 +744,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // lane takes new work at the next claim
         if constexpr (kBall) {
             if (A.ball_waves > 0 && A.cell_n > 0) {
+                // inside the ball, and not a ray leaving it from its surface (a refraction out of
+                // the glass, a reflection off it): the cell would not decide those
                 const V3 oc = sub(r.o, mk(A.cell_c[0], A.cell_c[1], A.cell_c[2]));
-                const bool inball = dot(oc, oc) < A.cell_r2;
+                const float o2 = dot(oc, oc);
+                const bool inball = o2 < A.cell_r2 && (o2 < A.cell_rin2 || dot(oc, r.d) < 0.f);
                 if (pool_push(ballrole ? 1 : 0, seg && (inball != ballrole))) {
                     phase = PH_IDLE;
                     item = 0xFFFFFFFFu;
@@ -752,8 +756,16 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             }
         }
         mark(3);
+        if (kProf) prof_iters++;
     }
     if (kProf && lane == 0) {
+        if (kBall) {   // RT_STAT_BALL in the profile variant: the ball waves' stage cycles and iterations
+            if (ballrole) {
+                for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_STAT_BALL + k], (unsigned long long)(prof[k] + (k == 3 ? prof[4] : 0)));
+                atomicAdd(&A.stats[RT_STAT_BALL + 4], (unsigned long long)prof_iters);
+            }
+            atomicAdd(&A.stats[RT_STAT_BALL + 5], (unsigned long long)prof_iters);
+        }
         // the scatter branches' cycles count in the shade stage too
         for (int k = 0; k < 4; ++k) atomicAdd(&A.stats[RT_STAT_PROF + k], (unsigned long long)(prof[k] + (k == 3 ? prof[4] : 0)));
         atomicAdd(&A.stats[RT_STAT_SHADE + 3], (unsigned long long)prof[4]);

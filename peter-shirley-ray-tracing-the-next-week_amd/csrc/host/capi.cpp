@@ -159,7 +159,7 @@ struct rt_scene {
     int nprescan = 0;             // BVH scenes: largest primitives tested in lockstep before the BVH
     // medium cell (rt_scene_create): primitives [cell_first, cell_first + cell_n) are copies of those near the ball
     int cell_first = 0, cell_n = 0;
-    float cell_c[3] = {0, 0, 0}, cell_r2 = 0;
+    float cell_c[3] = {0, 0, 0}, cell_r2 = 0, cell_rin2 = 0;
     int ngroups = 0;
     uint32_t root = 0;
     int has_bvh = 0, nmedia = 0, bvh_depth = 0, nnodes = 0, nprims = 0, bvh_width = 2, ninstances = 0;
@@ -504,8 +504,9 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             best_density = m.density;
             s->cell_n = (int)near.size();
             for (int k = 0; k < 3; k++) s->cell_c[k] = (float)c[k];
-            const double rk = R + mg / 2;
+            const double rk = R + mg / 2, rin = R * (1 - 1.0 / 1024);
             s->cell_r2 = (float)(rk * rk);
+            s->cell_rin2 = (float)(rin * rin);   // (routing only: rays nearer the surface count as inside when heading in)
             cell = near;
         }
         s->cell_first = (int)order.size();
@@ -886,6 +887,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.cell_n = s->cell_n;
     for (int k = 0; k < 3; k++) a.cell_c[k] = s->cell_c[k];
     a.cell_r2 = s->cell_r2;
+    a.cell_rin2 = s->cell_rin2;
     a.ball_waves = ball_waves();
     a.ball_batch = env_int("RTNW_BALL_BATCH", RT_BALL_BATCH, 1, 64);
     a.ball_claim = env_int("RTNW_BALL_CLAIM", RT_BALL_CLAIM, 0, 64);
@@ -1045,6 +1047,14 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         if (prof) {
             unsigned long long c[RT_STATS_LEN];
             HIP_TRY(hipMemcpy(c, s->stats, sizeof c, hipMemcpyDeviceToHost));
+            if (std::getenv("RTNW_TRACE")) {   // the ball waves' share of the stage cycles (diagnostics only)
+                const unsigned long long *b = c + RT_STAT_BALL;
+                std::fprintf(stderr,
+                             "rtnw ball waves (profile): iterations %llu of %llu; cycles claim %llu of %llu, traverse %llu of "
+                             "%llu, media %llu of %llu, shade %llu of %llu\n",
+                             b[4], b[5], b[0], c[RT_STAT_PROF], b[1], c[RT_STAT_PROF + 1], b[2], c[RT_STAT_PROF + 2], b[3],
+                             c[RT_STAT_PROF + 3]);
+            }
             stats->cycles_claim = (double)c[RT_STAT_PROF + 0];
             stats->cycles_traverse = (double)c[RT_STAT_PROF + 1];
             stats->cycles_media = (double)c[RT_STAT_PROF + 2];

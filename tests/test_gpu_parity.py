@@ -578,3 +578,31 @@ def test_ball_waves_leave_the_image_bitwise_unchanged(monkeypatch):
     for (x0, y0) in ((72, 40), (0, 0), (152, 112)):   # the subsurface sphere's pixels, and corners
         o = oracle_render("final", nx, ny, ns, seed=33, chunk=1, rect=(x0, y0, 8, 8))
         assert_exact(pixel_exact(ref[y0:y0 + 8, x0:x0 + 8], o))
+
+
+def test_deep_first_claims_with_chunks_batches_and_cameras(monkeypatch):
+    """Deep pixels first (capi.cpp prepare_job: the pixels whose primary rays enter a dense
+    medium are claimed first; each pre-made sample start carries its (chunk, job pixel)):
+    with chunks of 2 samples, a slab budget of 3 chunks per launch (several batches, so
+    c1 - c0 < nchunks_total), two cameras on one scene object (the job cache is keyed by
+    the camera) and a multi-tile job, the image is the same bit for bit with
+    RTNW_DEEP_FIRST=1 and =0, and the oracle's."""
+    nx, ny, ns = 96, 72, 12
+    sc = rtnw.Scene.builtin("final")
+    cams = [rtnw.Camera.preset("cornell", nx, ny), rtnw.Camera.preset("final_alt", nx, ny)]
+    p = rtnw.RenderParams(nx, ny, ns, seed=17, chunk=2)
+    tiles = [(0, 0, 48, 72), (48, 0, 48, 40), (48, 40, 48, 32)]
+    monkeypatch.setenv("RTNW_SLAB_BUDGET", str(nx * ny * 12 * 3))   # 3 chunks of 2 samples per launch
+    out = {}
+    for deep in ("1", "0"):
+        monkeypatch.setenv("RTNW_DEEP_FIRST", deep)
+        for ci, cam in enumerate(cams):
+            img = np.zeros((ny, nx, 3), np.float32)
+            for (x0, y0, w, h) in tiles:
+                img[y0:y0 + h, x0:x0 + w] = sc.render_tile(cam, p, x0, y0, w, h)
+            out[(deep, ci)] = img
+    for ci in range(2):
+        assert np.array_equal(out[("1", ci)].view(np.uint32), out[("0", ci)].view(np.uint32)), ci
+    assert not np.array_equal(out[("1", 0)], out[("1", 1)])   # the cameras differ
+    o = oracle_render("final", nx, ny, ns, seed=17, chunk=2, rect=(40, 24, 16, 16))
+    assert_exact(pixel_exact(out[("1", 0)][24:40, 40:56], o))

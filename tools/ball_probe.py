@@ -21,6 +21,8 @@ p = rtnw.RenderParams(500, 500, {args.spp}, seed=2024, flags=rtnw.RT_FLAG_COUNT)
 img, st = sc.render_tile(cam, p, 0, 0, 500, 500, stats=True)
 print('segments/sample %.3f node visits/segment %.3f kernel %.2f ms' % (st['segments'] / st['samples'],
       st['node_visits'] / st['segments'], st['kernel_ms']))
+p = rtnw.RenderParams(500, 500, {args.spp}, seed=2024, flags=rtnw.RT_FLAG_PROFILE)
+img, st = sc.render_tile(cam, p, 0, 0, 500, 500, stats=True)
 """
 for w in args.waves.split(","):
     env = dict(os.environ, RTNW_BALL_WAVES=w, RTNW_TRACE="1")
