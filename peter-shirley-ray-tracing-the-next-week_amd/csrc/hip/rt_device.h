@@ -769,6 +769,22 @@ struct LdsNodes {   // node references are byte offsets (n * 16, kSplit: n * 4) 
 __device__ __forceinline__ uint32_t &stk_at(uint32_t *stk, int sp) {   // one shift-add per address
     return *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(stk) + ((uint32_t)sp << 8));
 }
+// The BVH2-in-LDS stacks hold 16-bit entries (round 6): [depth][lane] of
+// int16, 128 B per depth level, half the LDS of 32-bit entries (final(): 56 -> 28 KiB per CU,
+// the room of the ball waves' path pools).  An interior reference there is a byte offset into
+// the node planes (< 16 KiB) and a leaf is encoded by the LDS copy as
+// 0xFFFF8000 | (count - 1) << 12 | first (first < 4096: rt_scene_create keeps scenes of more
+// primitives out of LDS), so an entry is the reference's low 16 bits and the sign-extending
+// read (ds_read_i16) restores it — no encode or decode instruction on a push or a pop.
+#define RT_LDS_LEAF16(ref) (0xFFFF8000u | ((RT_LEAF_COUNT(ref) - 1u) << 12) | RT_LEAF_FIRST(ref))
+#define RT_LDS_LEAF16_FIRST(ref) ((ref) & 0xFFFu)
+#define RT_LDS_LEAF16_COUNT(ref) ((((ref) >> 12) & 0x7u) + 1u)
+__device__ __forceinline__ void stk16_put(uint32_t *stk, int sp, uint32_t v) {
+    *reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(stk) + ((uint32_t)sp << 7)) = (uint16_t)v;
+}
+__device__ __forceinline__ uint32_t stk16_get(uint32_t *stk, int sp) {
+    return (uint32_t)(int32_t) * reinterpret_cast<int16_t *>(reinterpret_cast<char *>(stk) + ((uint32_t)sp << 7));
+}
 
 // 8-wide node step's tail: the nearest hit child (the first one in slot order on
 // ties) is the next node, the other hit children are pushed in reverse slot order.
@@ -813,7 +829,7 @@ __device__ __forceinline__ uint32_t node_step(const Nodes &src, uint32_t node, c
         const bool lt = tn1 < tn0;
         const bool second = h1 & (!h0 | lt);
         const uint32_t nearc = second ? c1 : (h0 ? c0 : RT_EMPTY_CHILD), farc = second ? c0 : c1;
-        stk_at(stk, sp) = farc;
+        stk16_put(stk, sp, farc);
         const int sp0 = h0 ? sp + RT_SP_UNIT : sp;
         sp = h1 ? sp0 : sp;
         return nearc;
@@ -952,7 +968,8 @@ __device__ __forceinline__ uint32_t descend(const Nodes &nodes, uint32_t &node, 
             node = park ? RT_EMPTY_CHILD : node;
             const bool pop = node == RT_EMPTY_CHILD && sp > 0;
             sp -= pop ? RT_SP_UNIT : 0;
-            const uint32_t top = stk_at(stk, sp);   // sp >= 0: pops only from a non-empty stack
+            // sp >= 0: pops only from a non-empty stack (LDS nodes: 16-bit entries)
+            const uint32_t top = std::is_same<Nodes, GlobalNodes>::value ? stk_at(stk, sp) : stk16_get(stk, sp);
             node = pop ? top : node;
         }
         if (__popcll(wballot(pleaf == RT_EMPTY_CHILD && node != RT_EMPTY_CHILD)) <= kTail) {
@@ -1402,6 +1419,9 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     asm volatile("" : "+v"(mca));
     const LogConsts lc = *(__attribute__((address_space(3))) const LogConsts *)(size_t)mca;
 #endif
+    // (An exp pre-test that skipped the double log for a wave of sure misses — u below
+    // 2^(-density D log2 e) (1 - 2^-12) — measured slower, round 6: c4 48.95 -> 49.45 ms, the
+    // share of 8 25.32 -> 25.63; a wave seldom holds only sure misses of both media.)
     const float hit_distance = (float)((double)neg_inv_density * log_f64(u48x(xk), lc));
     const bool hit = ok && hit_distance < distance_inside_boundary;
     const float tm = r1 + div_by(hit_distance, rd);

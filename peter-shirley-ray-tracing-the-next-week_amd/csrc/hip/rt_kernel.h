@@ -13,7 +13,8 @@
 #define RT_LDS_NODE_CAP 1024
 #define RT_LDS_NODE_BYTES (4 * RT_LDS_NODE_CAP * 16)
 #define RT_LDS_NODE_BYTES_MEDIA (14 * RT_LDS_NODE_CAP * 4)   // the media variants' dword planes (rt_device.h RtSplit)
-#define RT_LDS_STACK_BYTES(depth) ((RT_LDS_BLOCK / 64) * (depth) * 64 * 4)
+#define RT_LDS_STACK_BYTES(depth) ((RT_LDS_BLOCK / 64) * (depth) * 64 * 2)   // 16-bit entries (rt_device.h stk16_*)
+#define RT_LDS_MAX_PRIMS 4096   // leaf references of the LDS copy hold 12-bit first primitives
 #define RT_LDS_BUDGET 163840   // LDS bytes per CU (160 KiB)
 
 // scene features a megakernel variant carries code for (rt_launch_megakernel)

@@ -67,10 +67,10 @@ namespace {
 // Path pools of the ball waves (stage 6): paths whose segment starts inside the medium
 // cell's ball, and paths that left it, waiting in LDS for a wave of their kind (80 B each)
 #ifndef RT_BALL_POOL
-#define RT_BALL_POOL 28
+#define RT_BALL_POOL 96
 #endif
 #ifndef RT_NORM_POOL
-#define RT_NORM_POOL 24
+#define RT_NORM_POOL 80
 #endif
 typedef unsigned U4p __attribute__((ext_vector_type(4)));
 
@@ -145,8 +145,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_dyn) + lds_node_bytes<kSplit>()) +
-                               wave * (uint32_t)A.stack_depth * 64u + lane
+    // (LDS variant: 16-bit entries, [wave][depth][lane], rt_device.h stk16_*)
+    uint32_t *stk = kLds ? reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_dyn) + lds_node_bytes<kSplit>() +
+                                                        (wave * (uint32_t)A.stack_depth * 64u + lane) * 2u)
                          : &lds_stack[kMode ? 0 : wave][0][lane];
     CoopSlot *slots = lds_slots[wave];
     uint64_t *pre_key = lds_pre_key[wave];
@@ -170,8 +171,9 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const float4 b0 = N[0], b1 = N[1], b2 = N[2];
             float4 cf = N[3];
             const uint32_t c0 = (uint32_t)fbits(cf.x), c1 = (uint32_t)fbits(cf.y);
-            cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? c0 : lds_node_ref<kSplit>(c0));
-            cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? c1 : lds_node_ref<kSplit>(c1));
+            // leaves in the 16-bit stack form (rt_device.h RT_LDS_LEAF16)
+            cf.x = __uint_as_float((c0 & RT_LEAF_BIT) ? RT_LDS_LEAF16(c0) : lds_node_ref<kSplit>(c0));
+            cf.y = __uint_as_float((c1 & RT_LEAF_BIT) ? RT_LDS_LEAF16(c1) : lds_node_ref<kSplit>(c1));
             if constexpr (kSplit) {   // one dword per node and plane (rt_device.h RtSplit)
                 float *P = reinterpret_cast<float *>(lds_dyn) + i;
                 constexpr uint32_t C = RT_LDS_NODE_CAP;
@@ -627,7 +629,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     else
                         pleaf = descend<kWidth, kCount, kInst ? 1 : RT_DESCEND_STEPS>(gnodes, node, sl, best_t, stk, sp, cnt, dry);
                     if (pleaf != RT_EMPTY_CHILD) {
-                        const uint32_t first = RT_LEAF_FIRST(pleaf), nleaf = RT_LEAF_COUNT(pleaf);
+                        const uint32_t first = kLds ? RT_LDS_LEAF16_FIRST(pleaf) : RT_LEAF_FIRST(pleaf),
+                                       nleaf = kLds ? RT_LDS_LEAF16_COUNT(pleaf) : RT_LEAF_COUNT(pleaf);
                         // primitives in pairs: both 32-B heads are fetched before either test
                         for (uint32_t q = 0; q < nleaf; q += 2) {
                             const uint32_t ia = first + q;

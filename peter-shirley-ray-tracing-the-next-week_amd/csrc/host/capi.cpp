@@ -675,7 +675,7 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
             lds_cu <= 0)
             lds_cu = 0;
         s->lds_nodes = want && !s->scan && s->bvh_width == 2 && s->has_bvh && !(s->root & RT_LEAF_BIT) &&
-                       s->nnodes <= RT_LDS_NODE_CAP &&
+                       s->nnodes <= RT_LDS_NODE_CAP && d->nprims < RT_LDS_MAX_PRIMS &&
                        need_actual <= std::min<long>(RT_LDS_BUDGET, lds_cu);
         if (s->lds_nodes)
             for (int mode = 0; mode < 3; mode++) s->grid[mode] = s->cus;
