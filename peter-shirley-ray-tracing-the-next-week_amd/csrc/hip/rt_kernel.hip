@@ -10,7 +10,8 @@
 //   material::scatter  material.h:16-151 ; texture::value texture.h:16-59 ; perlin.h:25-74
 //
 // Execution model (wave64, CDNA4):
-//   * persistent workgroups of 4 waves; each LANE owns one camera path at a time and
+//   * persistent workgroups (16 waves, one per CU, with the BVH2 in LDS; 4 waves with
+//     it in HBM; 4 for the flat scan); each LANE owns one camera path at a time and
 //     regenerates a new camera sample as soon as its path terminates, so lanes stay
 //     busy across bounces (path regeneration) instead of idling until the longest
 //     path of the wave finishes;
@@ -23,7 +24,12 @@
 //     float atomics, independent of the number of GPUs; with one sample per item
 //     it is the reference's own `col += temp` order);
 //   * the BVH traversal stack lives in LDS, laid out [wave][depth][lane] so every
-//     push/pop of a wave is one conflict-free ds_write_b32/ds_read_b32;
+//     push/pop of a wave is one conflict-free LDS access (16-bit entries with the BVH2
+//     in LDS, rt_device.h stk16_*);
+//   * ball waves (stage 6, final()'s variant): the workgroup's last A.ball_waves waves
+//     gather, through two LDS path pools, the paths whose segments start inside the
+//     dense medium's ball, whose closest-hit searches end at the medium cell's few
+//     primitives without a BVH descent, so those waves skip the traversal stage;
 //   * nodes, primitives and materials are 16-B records read with dwordx4 loads.
 //
 // Arithmetic follows the reference's float/double promotions; the file is compiled
@@ -1022,7 +1028,8 @@ extern "C" long rt_lds_need_bytes(int features, int stack_depth) {
     case RT_FEAT_CHECKER | RT_FEAT_PRESCAN: stat = lds_static_of<RT_FEAT_CHECKER | RT_FEAT_PRESCAN>(); break;
     default: stat = lds_static_of<RT_FEAT_ALL>(); break;
     }
-    stat = std::max(stat, rt_megakernel_lds_static_bytes());
+    // (the ball waves' path pools: final()'s variant only, rt_megakernel kBall)
+    stat = std::max(stat, rt_megakernel_lds_static_bytes() + (v == RT_FEAT_MEDIA ? (RT_BALL_POOL + RT_NORM_POOL - 2) * 80 : 0));
     const long nodes = rt_lds_split(1, v, 2) ? lds_node_bytes<1>() : lds_node_bytes<0>();
     return (long)stat + nodes + (long)RT_LDS_STACK_BYTES((long)stack_depth);
 }
@@ -1030,6 +1037,6 @@ extern "C" long rt_lds_need_bytes(int features, int stack_depth) {
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 + 16 +
-                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8 + 8) + RT_LCG_JUMPS * 16) + 256;
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8 + 8) + RT_LCG_JUMPS * 16 + 2 * 80 + 16) + 256;
 }
 #endif  // RT_KNOB_CHECK
