@@ -531,7 +531,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // the pool is dry and few paths are left: the launch's end waits on their latency
         const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
         {
-            const bool starting = phase == PH_IDLE && !finished && item != 0xFFFFFFFFu;
+            const bool starting = phase == PH_IDLE && !finished && (!kBall || item != 0xFFFFFFFFu);
             float cu_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f, cv_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f;   // starting lanes only
             camera_begin(starting, cu_, cv_);
             const V3 disk = coop_reject<2, kCount>(starting, g, slots, jt, lane, cnt, DiskCand());
@@ -722,7 +722,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (ends) end_path(mul(beta, shade_emitted(A, have, r, rd, st)));
         retire_and_claim(false);
         // (a lane left without work by a ball wave's claim, waiting for the pool, has no item)
-        const bool starting = phase == PH_IDLE && !finished && item != 0xFFFFFFFFu;
+        const bool starting = phase == PH_IDLE && !finished && (!kBall || item != 0xFFFFFFFFu);
         float cu_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f, cv_ = (RT_SHADE_LEAN & 8) ? unset_f() : 0.f;   // starting lanes only
         camera_begin(starting, cu_, cv_);
         // material.h:41-47 for the scattering lanes, camera.h:6-12 for the new samples
