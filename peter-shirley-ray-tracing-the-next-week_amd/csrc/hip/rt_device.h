@@ -1420,8 +1420,10 @@ __device__ __forceinline__ void medium_one(const RtKernelArgs &A, const MediumRe
     const LogConsts lc = *(__attribute__((address_space(3))) const LogConsts *)(size_t)mca;
 #endif
     // (An exp pre-test that skipped the double log for a wave of sure misses — u below
-    // 2^(-density D log2 e) (1 - 2^-12) — measured slower, round 6: c4 48.95 -> 49.45 ms, the
-    // share of 8 25.32 -> 25.63; a wave seldom holds only sure misses of both media.)
+    // 2^(-density D log2 e) (1 - 2^-12) — measured slower, round 6: in every wave c4 48.95 ->
+    // 49.45 ms, the share of 8 25.32 -> 25.63 (a wave seldom holds only sure misses of both
+    // media); in the ball waves only, where final()'s fog after the dense medium's scatter
+    // almost never scatters, 48.88 -> 49.17 and 25.19 -> 25.45: profiles/r06/pretest*_ab.log.)
     const float hit_distance = (float)((double)neg_inv_density * log_f64(u48x(xk), lc));
     const bool hit = ok && hit_distance < distance_inside_boundary;
     const float tm = r1 + div_by(hit_distance, rd);
