@@ -348,7 +348,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         const uint64_t M = wballot(want);
         if (M == 0ull) return false;
         const uint32_t cap = k == 0 ? RT_BALL_POOL : RT_NORM_POOL;
-        if (pool_peek(k) >= cap) return false;
+        if (pool_peek(k) >= cap) {
+            if (kCount && k == 0 && lane == 0) cnt.ball[RT_BALL_DENIED] += (uint64_t)__popcll(M);
+            return false;
+        }
         pool_lock();
         const uint32_t n = __builtin_amdgcn_readfirstlane(((LdsVU *)lds_pool_ctl)[1 + k]);
         const uint32_t take = min((uint32_t)__popcll(M), cap - min(n, cap));
@@ -364,7 +367,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         }
         if (lane == 0) ((LdsVU *)lds_pool_ctl)[1 + k] = n + take;
         pool_unlock();
-        if (kCount && lane == 0) cnt.ball[k == 0 ? RT_BALL_PUSH_IN : RT_BALL_PUSH_OUT] += take;
+        if (kCount && lane == 0) {
+            cnt.ball[k == 0 ? RT_BALL_PUSH_IN : RT_BALL_PUSH_OUT] += take;
+            if (k == 0) cnt.ball[RT_BALL_DENIED] += (uint64_t)__popcll(M) - take;
+        }
         return go;
     };
     // lanes with `need` take paths from pool k (a fresh segment each); returns who took one
@@ -430,9 +436,11 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             if (ballrole && !exhausted) {
                 // a ball wave claims new samples only while fewer than A.ball_claim of its lanes
                 // hold a path, and outside the top only with its pool empty (its idle lanes wait
-                // for the pool's paths at the next top); lanes left idle have no item
+                // for the pool's paths at the next top); lanes left idle have no item.  A wave
+                // with no path at all always claims at the top: only a claim finds the pool
+                // exhausted, and a wave that never did would never leave the kernel.
                 const uint32_t busy = (uint32_t)__popcll(wballot(!(phase == PH_IDLE && item == 0xFFFFFFFFu)));
-                if ((!top && pool_peek(0) != 0u) || busy >= (uint32_t)A.ball_claim) return;
+                if ((!top && pool_peek(0) != 0u) || (busy >= (uint32_t)A.ball_claim && !(top && busy == 0u))) return;
             }
         }
         uint64_t need_mask = wballot(need);
@@ -603,7 +611,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                     if (in && best_t < tsafe) phase = PH_READY;
                     if (kCount) {
                         const uint64_t decided = wballot(in && phase == PH_READY);
-                        if (lane == 0) cnt.ball[ballrole ? RT_BALL_CELL_BALL : RT_BALL_CELL_OTHER] += (uint64_t)__popcll(decided);
+                        if (lane == 0) cnt.ball[RT_BALL_CELL_BALL] += (uint64_t)__popcll(decided);
                     }
                 }
             }

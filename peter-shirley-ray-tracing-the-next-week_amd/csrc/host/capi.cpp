@@ -890,7 +890,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.cell_rin2 = s->cell_rin2;
     a.ball_waves = ball_waves();
     a.ball_batch = env_int("RTNW_BALL_BATCH", RT_BALL_BATCH, 1, 64);
-    a.ball_claim = env_int("RTNW_BALL_CLAIM", RT_BALL_CLAIM, 0, 64);
+    a.ball_claim = env_int("RTNW_BALL_CLAIM", RT_BALL_CLAIM, 1, 64);
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = scene_features(s);
@@ -1037,11 +1037,11 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
                 HIP_TRY(hipMemcpy(b, (unsigned long long *)s->stats + RT_STAT_BALL, sizeof b, hipMemcpyDeviceToHost));
                 std::fprintf(stderr,
                              "rtnw ball waves: iterations %llu, live lanes / iteration %.1f, traversal rounds / iteration %.2f, "
-                             "cell-decided segments in ball waves %llu, in other waves %llu (of %.0f), pushed in %llu, "
+                             "cell-decided segments in ball waves %llu, pushes refused (pool full) %llu (of %.0f segments), pushed in %llu, "
                              "pushed out %llu, taken %llu\n",
                              b[RT_BALL_ITERS], b[RT_BALL_ITERS] ? (double)b[RT_BALL_LIVE] / b[RT_BALL_ITERS] : 0.0,
                              b[RT_BALL_ITERS] ? (double)b[RT_BALL_ROUNDS] / b[RT_BALL_ITERS] : 0.0, b[RT_BALL_CELL_BALL],
-                             b[RT_BALL_CELL_OTHER], stats->segments, b[RT_BALL_PUSH_IN], b[RT_BALL_PUSH_OUT], b[RT_BALL_TAKEN]);
+                             b[RT_BALL_DENIED], stats->segments, b[RT_BALL_PUSH_IN], b[RT_BALL_PUSH_OUT], b[RT_BALL_TAKEN]);
             }
         }
         if (prof) {

@@ -165,7 +165,7 @@ enum {
     RT_STATS_LEN = RT_CNT_N + 28
 };
 // ball-wave counters: ball-wave iterations, their live lanes and traversal rounds summed over
-// them, segments the medium cell decided in ball / other waves, paths pushed into the ball's
-// pool / the others' pool, paths taken from either
-enum { RT_BALL_ITERS = 0, RT_BALL_LIVE, RT_BALL_ROUNDS, RT_BALL_CELL_BALL, RT_BALL_CELL_OTHER, RT_BALL_PUSH_IN,
+// them, segments the medium cell decided (in ball waves), paths a normal wave could not push
+// (the ball's pool full), paths pushed into the ball's pool / the others' pool, paths taken
+enum { RT_BALL_ITERS = 0, RT_BALL_LIVE, RT_BALL_ROUNDS, RT_BALL_CELL_BALL, RT_BALL_DENIED, RT_BALL_PUSH_IN,
        RT_BALL_PUSH_OUT, RT_BALL_TAKEN, RT_BALL_N };

@@ -30,7 +30,7 @@ for r in range(args.rounds):
             env[k] = v
         out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
                               "--spp", str(args.spp), "--no-cpu-baseline"] + list(filter(None, bargs.split("+"))), env=env, capture_output=True, text=True,
-                             timeout=600)
+                             timeout=int(os.environ.get("AB_RUN_TIMEOUT", "150")))
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if not line:
             print(lib, "FAILED", out.stderr[-2000:], flush=True)
