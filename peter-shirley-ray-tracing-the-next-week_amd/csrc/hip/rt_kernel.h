@@ -54,7 +54,8 @@ struct RtKernelArgs {
     float cell_rin2;          //     ... and the squared radius inside which a ray counts as inside whatever its direction
     int ball_waves;           // waves per workgroup that take the medium cell's paths first (LDS media variant) ...
     int ball_batch;           //     ... their ready batch (the others': RT_READY_BATCH) ...
-    int ball_claim;           //     ... and the busy lanes below which they claim new samples
+    int ball_claim;           //     ... and the busy lanes below which they claim new samples ...
+    int ball_park;            //     ... and whether their segments the cell does not decide move to normal waves
     int lds_nodes;          // 1: BVH2 nodes copied to LDS (RT_LDS_BLOCK workgroups, one per CU)
     int stack_depth;        // traversal stack entries per lane of the LDS variant (BVH depth + 1)
     // camera (camera.h members)

@@ -87,7 +87,9 @@ typedef unsigned U4p __attribute__((ext_vector_type(4)));
 // kCount: visit counters (RT_FLAG_COUNT).  kProf: wave-level s_memtime stamps per
 // stage (RT_FLAG_PROFILE, a diagnostic build whose timing is never quoted).
 // Lane phases of the batched state machine below.
-enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2 };
+// PH_PARK (ball waves): a new segment the medium cell did not decide, waiting for stage 6 to
+// move it to a normal wave instead of traversing here
+enum : int { PH_IDLE = 0, PH_TRAV = 1, PH_READY = 2, PH_PARK = 3 };
 
 // kFeat (RT_FEAT_*): the scene features the variant carries code for — instance
 // chains (cornell scenes), (u, v)-reading materials (earth()), checker textures
@@ -593,7 +595,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             if (kCell && ballrole && A.cell_n > 0) {
                 bool in = false;
                 float tsafe = 0.f;
-                if (fresh && phase == PH_TRAV) {
+                const bool fr = fresh && phase == PH_TRAV;
+                if (fr) {
                     const V3 oc = sub(r.o, mk(A.cell_c[0], A.cell_c[1], A.cell_c[2]));
                     const float a = dot(r.d, r.d), b = dot(oc, r.d), cc = dot(oc, oc) - A.cell_r2;
                     if (cc < 0.f && a > 0.f) {
@@ -614,6 +617,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                         if (lane == 0) cnt.ball[RT_BALL_CELL_BALL] += (uint64_t)__popcll(decided);
                     }
                 }
+                // a new segment the cell did not decide waits for stage 6 to leave for a normal
+                // wave (A.ball_park): a ball wave's few traversing lanes ran its traversal rounds
+                // at a few lanes each.  Not once the claims are exhausted: a ball wave then takes
+                // the other pool's paths too, and parking them again could pass a path between
+                // the pool and a ball wave forever when no normal wave is left
+                if (A.ball_park && !exhausted && fr && phase == PH_TRAV) phase = PH_PARK;
             }
             // pre-scan: the scene's largest primitives (capi.cpp), kept out of the BVH,
             // tested in lockstep by every lane with a new segment before its descent;
@@ -766,9 +775,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 const V3 oc = sub(r.o, mk(A.cell_c[0], A.cell_c[1], A.cell_c[2]));
                 const float o2 = dot(oc, oc);
                 const bool inball = o2 < A.cell_r2 && (o2 < A.cell_rin2 || dot(oc, r.d) < 0.f);
-                if (pool_push(ballrole ? 1 : 0, seg && (inball != ballrole))) {
+                const bool parked = phase == PH_PARK;
+                if (pool_push(ballrole ? 1 : 0, (seg && (inball != ballrole)) || parked)) {
                     phase = PH_IDLE;
                     item = 0xFFFFFFFFu;
+                } else if (parked) {
+                    phase = PH_TRAV;   // the pool is full: it traverses here after all
                 }
             }
         }

@@ -572,6 +572,18 @@ def test_ball_waves_leave_the_image_bitwise_unchanged(monkeypatch):
     batched = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=33), 0, 0, nx, ny)
     assert np.array_equal(batched.view(np.uint32), ref.view(np.uint32))
     monkeypatch.delenv("RTNW_SLAB_BUDGET")
+    # ball waves that traverse their undecided segments themselves, that claim new samples
+    # only when wholly idle, on a job of one 8 x 8 block (the claims exhausted at once)
+    for env in ({"RTNW_BALL_PARK": "0"}, {"RTNW_BALL_CLAIM": "1"}, {"RTNW_BALL_WAVES": "16", "RTNW_BALL_CLAIM": "1"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        img = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=33), 0, 0, nx, ny)
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), env
+        tiny = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=33), 72, 40, 8, 8)
+        assert np.array_equal(tiny.view(np.uint32), ref[40:48, 72:80].view(np.uint32)), env
+        for k in env:
+            monkeypatch.delenv(k)
+    monkeypatch.setenv("RTNW_BALL_WAVES", "3")
     monkeypatch.setenv("RTNW_CELL", "0")
     nocell = rtnw.Scene.builtin("final").render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=33), 0, 0, nx, ny)
     assert np.array_equal(nocell.view(np.uint32), ref.view(np.uint32))
