@@ -528,7 +528,9 @@ __device__ __forceinline__ float boundary_t(const float4 *B, const float4 *insts
 // ----------------------------------------------------------------- Perlin
 // One noise() (perlin.h:43-61, 25-39).  The six permutation reads are issued
 // together, then the eight gradient reads: two memory round trips per call.
-__device__ __forceinline__ float perlin_noise(const float4 *ranvec, const int *perm, V3 p) {
+// (RV / PM: the tables' pointer types — global memory, or final()'s variant's LDS copies)
+template <class RV, class PM>
+__device__ __forceinline__ float perlin_noise(RV ranvec, PM perm, V3 p) {
     float u = p.x - floorf(p.x);
     float v = p.y - floorf(p.y);
     float w = p.z - floorf(p.z);
@@ -550,7 +552,7 @@ __device__ __forceinline__ float perlin_noise(const float4 *ranvec, const int *p
         V3 g[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const float4 t = ranvec[px[a] ^ py[c >> 1] ^ pz[c & 1]];
+            const auto t = ranvec[px[a] ^ py[c >> 1] ^ pz[c & 1]];
             g[c] = mk(t.x, t.y, t.z);
         }
 #pragma unroll
@@ -1149,7 +1151,8 @@ __device__ __forceinline__ V3 coop_reject_mixed(bool want, bool disk, Rng &g, Co
 // reference's loop does.  A wave with one noisy lane used to run all 7 octaves as
 // a chain of 28 dependent gathers; now it runs one noise() per round.
 // Must be called with all 64 lanes of the wave active.
-__device__ __forceinline__ float coop_turb(bool want, V3 q, const float4 *ranvec, const int *perm, CoopSlot *slots,
+template <class RV, class PM>
+__device__ __forceinline__ float coop_turb(bool want, V3 q, RV ranvec, PM perm, CoopSlot *slots,
                                            uint32_t lane) {
     const uint64_t U = wballot(want);
     if (U == 0ull) return 0.f;
@@ -1484,9 +1487,9 @@ struct ShadeState {
 
 // Material, depth test, texture value incl. cooperative turbulence (textures
 // texture.h / perlin.h).  Must be called with all 64 lanes of the wave active.
-template <bool kCount, bool kUV = true, bool kChecker = true>
+template <bool kCount, bool kUV = true, bool kChecker = true, class RV = const float4 *, class PM = const int *>
 __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool ready, bool have, const Hit &hr, int depth,
-                                                  CoopSlot *slots, uint32_t lane, Counters &cnt) {
+                                                  CoopSlot *slots, uint32_t lane, Counters &cnt, RV ranvec, PM perm) {
     const bool shading = ready && have;
     ShadeState st;
     st.kind = -1;
@@ -1512,7 +1515,7 @@ __device__ __forceinline__ ShadeState shade_begin(const RtKernelArgs &A, bool re
         }
     }
     if (kCount && noisy) cnt.noise++;
-    const float turb = coop_turb(noisy, scale(nscale, hr.p), A.ranvec, A.perm, slots, lane);   // perlin.h:64-74
+    const float turb = coop_turb(noisy, scale(nscale, hr.p), ranvec, perm, slots, lane);   // perlin.h:64-74
     if (noisy) {                                                                               // texture.h:52-56
         const float sv = 1 + rt_sinf(nscale * hr.p.x + 5 * turb);
         const float h = 0.5f * 1;

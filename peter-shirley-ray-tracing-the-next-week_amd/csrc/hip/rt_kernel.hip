@@ -73,10 +73,10 @@ namespace {
 // Path pools of the ball waves (stage 6): paths whose segment starts inside the medium
 // cell's ball, and paths that left it, waiting in LDS for a wave of their kind (80 B each)
 #ifndef RT_BALL_POOL
-#define RT_BALL_POOL 96
+#define RT_BALL_POOL 80
 #endif
 #ifndef RT_NORM_POOL
-#define RT_NORM_POOL 80
+#define RT_NORM_POOL 64
 #endif
 typedef unsigned U4p __attribute__((ext_vector_type(4)));
 
@@ -149,6 +149,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ U4p lds_pool_in[kBall ? RT_BALL_POOL : 1][5];
     __shared__ U4p lds_pool_out[kBall ? RT_NORM_POOL : 1][5];
     __shared__ uint32_t lds_pool_ctl[4];
+    // (kBall) Perlin's tables (perlin.h:76-79: 256 gradients, 3 x 256 permutations), 7 KiB of
+    // the LDS the 16-bit stacks left: the noise texture's dependent gathers from LDS
+    __shared__ F4v lds_ranvec[kBall ? 256 : 1];
+    __shared__ int lds_perm[kBall ? 768 : 1];
     extern __shared__ float4 lds_dyn[];   // kLds: node planes, then the stacks
     const uint32_t lane = lane_id();
     // the wave's index in the workgroup is wave-uniform: its LDS bases live in SGPRs
@@ -169,6 +173,13 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         lds_mconst = LogConsts{1.0 / 7, -1.0 / 6, 0.2, -0.25, 1.0 / 3};
     }
     for (uint32_t i = threadIdx.x; i < RT_LCG_JUMPS; i += kBlock) lds_jump[i] = kLcgJump.e[i];
+    if (kBall) {
+        for (uint32_t i = threadIdx.x; i < 256; i += kBlock) {
+            const float4 v = A.ranvec[i];
+            lds_ranvec[i] = F4v{v.x, v.y, v.z, v.w};
+        }
+        for (uint32_t i = threadIdx.x; i < 768; i += kBlock) lds_perm[i] = A.perm[i];
+    }
     rtl_lds_init(threadIdx.x);   // rt_libm.h's sine constants
     const LdsJump *jt = (const LdsJump *)lds_jump;
     if (kLds) {
@@ -723,7 +734,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // the depth limit) add their radiance, retire, claim and draw their next camera
         // sample's jitter right here, so that the new samples' lens-disk candidates run
         // in the same cooperative rounds as the scattering lanes' sphere candidates.
-        const ShadeState st = shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt);
+        typedef __attribute__((address_space(3))) const F4v LdsRanvec;
+        typedef __attribute__((address_space(3))) const int LdsPerm;
+        const ShadeState st = kBall ? shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt,
+                                                                         (LdsRanvec *)lds_ranvec, (LdsPerm *)lds_perm)
+                                    : shade_begin<kCount, kUV, kChecker>(A, ready, have, hr, depth, slots, lane, cnt,
+                                                                         A.ranvec, A.perm);
         const bool ends = shade_ends(ready, have, st);
         if (kCount) {   // material divergence: the scatter branches this wave pass runs (shade_finish)
             const bool sc = ready && !ends;
@@ -1048,8 +1064,9 @@ extern "C" long rt_lds_need_bytes(int features, int stack_depth) {
     case RT_FEAT_CHECKER | RT_FEAT_PRESCAN: stat = lds_static_of<RT_FEAT_CHECKER | RT_FEAT_PRESCAN>(); break;
     default: stat = lds_static_of<RT_FEAT_ALL>(); break;
     }
-    // (the ball waves' path pools: final()'s variant only, rt_megakernel kBall)
-    stat = std::max(stat, rt_megakernel_lds_static_bytes() + (v == RT_FEAT_MEDIA ? (RT_BALL_POOL + RT_NORM_POOL - 2) * 80 : 0));
+    // (the ball waves' path pools and Perlin's tables: final()'s variant only, rt_megakernel kBall)
+    stat = std::max(stat, rt_megakernel_lds_static_bytes() +
+                              (v == RT_FEAT_MEDIA ? (RT_BALL_POOL + RT_NORM_POOL - 2) * 80 + 255 * 16 + 767 * 4 : 0));
     const long nodes = rt_lds_split(1, v, 2) ? lds_node_bytes<1>() : lds_node_bytes<0>();
     return (long)stat + nodes + (long)RT_LDS_STACK_BYTES((long)stack_depth);
 }
@@ -1057,6 +1074,6 @@ extern "C" long rt_lds_need_bytes(int features, int stack_depth) {
 // the LDS variant's static arrays: stack placeholder, cooperative slots, media, camera
 extern "C" int rt_megakernel_lds_static_bytes(void) {
     return (int)(4 * 64 + (RT_LDS_BLOCK / 64) * 64 * sizeof(CoopSlot) + RT_LDS_MEDIA * sizeof(MediumRec) + 6 * 16 + 16 +
-                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8 + 8) + RT_LCG_JUMPS * 16 + 2 * 80 + 16) + 256;
+                 (RT_LDS_BLOCK / 64) * RT_PRE * (8 + 8 + 8) + RT_LCG_JUMPS * 16 + 2 * 80 + 16 + 16 + 4) + 256;
 }
 #endif  // RT_KNOB_CHECK
