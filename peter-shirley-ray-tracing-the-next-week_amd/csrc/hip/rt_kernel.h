@@ -25,6 +25,8 @@
 #define RT_FEAT_MEDIA 16    // constant_medium (without it: no media stage, no medium-stream key per sample)
 #define RT_FEAT_ALL 31
 
+#define RT_WAVE_LOG_WORDS 8
+
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)
     const float4 *nodes;    // BVH nodes, breadth-first: 4 / 8 / 16 / 8 x float4 (width 2 / 4 / 8 / RT_BVH_CW8)
@@ -56,6 +58,8 @@ struct RtKernelArgs {
     int ball_batch;           //     ... their ready batch (the others': RT_READY_BATCH) ...
     int ball_claim;           //     ... and the busy lanes below which they claim new samples ...
     int ball_park;            //     ... and whether their segments the cell does not decide move to normal waves
+    int ball_drain;           //     ... and whether, with the claims exhausted, normal waves leave the ball's pool to them
+    int dry_batch;            // a dry wave's ready batch (RT_DRY_LANES live lanes or fewer; 64: the normal one)
     int lds_nodes;          // 1: BVH2 nodes copied to LDS (RT_LDS_BLOCK workgroups, one per CU)
     int stack_depth;        // traversal stack entries per lane of the LDS variant (BVH depth + 1)
     // camera (camera.h members)
@@ -81,7 +85,9 @@ struct RtKernelArgs {
     float *slab;              // [nchunks][npix] partial sums (rgb, rt_slab_floats() floats each) of this batch
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)
-    unsigned long long *wave_log;   // profile variant, RTNW_WAVE_LOG: per wave (start, dry, end, hw id, items)
+    // profile variant, RTNW_WAVE_LOG: RT_WAVE_LOG_WORDS per wave (start, dry, end, hw id, items,
+    // iterations after dry, live lanes summed over them, paths taken from the pools after dry)
+    unsigned long long *wave_log;
 };
 
 extern "C" hipError_t rt_launch_megakernel(const RtKernelArgs *a, int grid, int mode, hipStream_t stream);

@@ -144,8 +144,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     __shared__ uint64_t lds_pre_key[kBlock / 64][RT_PRE];
     __shared__ float2 lds_pre_uv[kBlock / 64][RT_PRE];
     __shared__ uint2 lds_pre_cp[kBlock / 64][RT_PRE];   // each entry's (sample chunk, job pixel)
-    // stage 6's path pools (kBall): [0] paths inside the ball, [1] paths outside; a lock and
-    // the two counts
+    // stage 6's path pools (kBall): [0] paths inside the ball, [1] paths outside; a lock, the
+    // two counts and the number of ball waves still running
     __shared__ U4p lds_pool_in[kBall ? RT_BALL_POOL : 1][5];
     __shared__ U4p lds_pool_out[kBall ? RT_NORM_POOL : 1][5];
     __shared__ uint32_t lds_pool_ctl[4];
@@ -168,7 +168,8 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     // the media records are read from LDS (one broadcast read per medium)
     if (kMedia) load_media<kBlock>(A, lds_media);
     if (threadIdx.x == 0) {
-        lds_pool_ctl[0] = lds_pool_ctl[1] = lds_pool_ctl[2] = lds_pool_ctl[3] = 0;
+        lds_pool_ctl[0] = lds_pool_ctl[1] = lds_pool_ctl[2] = 0;
+        lds_pool_ctl[3] = kBall ? (uint32_t)min(max(A.ball_waves, 0), kBlock / 64) : 0u;
         store_camera(A, lds_cam);
         lds_mconst = LogConsts{1.0 / 7, -1.0 / 6, 0.2, -0.25, 1.0 / 3};
     }
@@ -250,6 +251,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     const uint64_t rt_start = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t rt_exhaust = 0;
     uint32_t rt_items = 0;   // work items this wave claimed (kProf)
+    uint64_t dr_iters = 0, dr_live = 0, dr_taken = 0;   // (kProf) after the dry point: iterations, live lanes, pooled paths taken
     auto mark = [&](int k) {
         if (kProf) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
@@ -344,6 +346,15 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     auto pool_peek = [&](int k) -> uint32_t {   // a racy hint; decisions are made under the lock
         return __builtin_amdgcn_readfirstlane(((LdsVU *)lds_pool_ctl)[1 + k]);
     };
+    // (A.ball_drain) with the claims exhausted a normal wave leaves the ball's paths to the ball
+    // waves while one runs: there the medium cell ends their searches (in a normal wave a ball
+    // path's segment took a full descent, in iterations that wait for the slowest lane: 17 us
+    // against 11 in the drain, profiles/r06/wave_drain*.json).  A ball wave leaves under the lock
+    // and lowers the count there, so a path pushed to the ball's pool after the last one left
+    // is seen by its pusher, which takes it back or stays until the pool is empty.
+    auto ball_pool_mine = [&]() -> bool {
+        return ballrole || !A.ball_drain || __builtin_amdgcn_readfirstlane(((LdsVU *)lds_pool_ctl)[3]) == 0u;
+    };
     auto pool_lock = [&]() {
         if (lane == 0)
             while (atomicCAS(&lds_pool_ctl[0], 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
@@ -413,6 +424,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (lane == 0) ((LdsVU *)lds_pool_ctl)[1 + k] = n - take;
         pool_unlock();
         if (kCount && lane == 0) cnt.ball[RT_BALL_TAKEN] += take;
+        if (kProf && exhausted) dr_taken += take;
         if (got) {
             finished = false;
             pre_have = false;
@@ -442,7 +454,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 need = phase == PH_IDLE && item == 0xFFFFFFFFu;
                 // pool 0 holds the ball's paths, 1 the others'; with the claims exhausted a
                 // wave whose own pool is empty takes from the other
-                const bool other = exhausted && pool_peek(ballrole ? 0 : 1) == 0u;
+                const bool other = exhausted && pool_peek(ballrole ? 0 : 1) == 0u && ball_pool_mine();
                 const int k = (other == ballrole) ? 1 : 0;
                 if (pool_take(k, need)) need = false;
             }
@@ -546,9 +558,20 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         // next sample inside stage 5)
         retire_and_claim(true);
         const uint64_t live = wballot(!finished);
-        // (kBall) a wave leaves only with both pools empty: paths another wave left there are
-        // taken by the next iteration's retire_and_claim (this one runs with no lane active)
-        if (live == 0ull && (!kBall || (pool_peek(0) | pool_peek(1)) == 0u)) break;
+        // (kBall) a wave leaves only with the pools it serves empty: paths another wave left there
+        // are taken by the next iteration's retire_and_claim (this one runs with no lane active).
+        // A ball wave serves both and decides under the lock (ball_pool_mine)
+        if (live == 0ull) {
+            if (!kBall) break;
+            if ((pool_peek(1) | (ball_pool_mine() ? pool_peek(0) : 0u)) == 0u) {
+                if (!ballrole) break;
+                pool_lock();
+                const bool leave = (pool_peek(0) | pool_peek(1)) == 0u;
+                if (leave && lane == 0) ((LdsVU *)lds_pool_ctl)[3] = ((LdsVU *)lds_pool_ctl)[3] - 1u;
+                pool_unlock();
+                if (leave) break;
+            }
+        }
         // the pool is dry and few paths are left: the launch's end waits on their latency
         const bool dry = exhausted && __popcll(live) <= RT_DRY_LANES;
         {
@@ -649,9 +672,14 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
                 cnt.ball[RT_BALL_ITERS]++;
                 cnt.ball[RT_BALL_LIVE] += (uint64_t)__popcll(live);
             }
+            const int batch = ballrole ? A.ball_batch : RT_READY_BATCH;
             for (;;) {
                 if (wballot(phase == PH_TRAV) == 0ull) break;
-                if (__popcll(wballot(phase == PH_READY)) >= (ballrole ? A.ball_batch : RT_READY_BATCH)) break;
+                // (A.dry_batch) a dry wave holds fewer lanes than the batch, and its iteration waits for
+                // the slowest lane's search (17 us in the drain against ~11 in the steady state,
+                // profiles/r06/wave_drain*.json): it shades once A.dry_batch lanes are ready
+                const uint32_t nready = (uint32_t)__popcll(wballot(phase == PH_READY));
+                if (nready >= (uint32_t)batch || (dry && nready >= (uint32_t)A.dry_batch)) break;
                 if (kCount && ballrole && lane == 0) cnt.ball[RT_BALL_ROUNDS]++;
                 if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
@@ -801,7 +829,10 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             }
         }
         mark(3);
-        if (kProf) prof_iters++;
+        if (kProf) {
+            prof_iters++;
+            if (exhausted) { dr_iters++; dr_live += (uint64_t)__popcll(live); }
+        }
     }
     if (kProf && lane == 0) {
         if (kBall) {   // RT_STAT_BALL in the profile variant: the ball waves' stage cycles and iterations
@@ -829,12 +860,15 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
         if (A.wave_log) {   // HW_ID (cu, simd, wave slot, se) and XCC_ID through s_getreg (reads)
             const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
             const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
-            unsigned long long *W = A.wave_log + 5 * ((size_t)blockIdx.x * (kBlock / 64) + wave);
+            unsigned long long *W = A.wave_log + RT_WAVE_LOG_WORDS * ((size_t)blockIdx.x * (kBlock / 64) + wave);
             W[0] = rt_start;
             W[1] = rt_exhaust ? rt_exhaust : rt_end;
             W[2] = rt_end;
             W[3] = ((unsigned long long)xcc << 32) | hw;
             W[4] = rt_items;
+            W[5] = dr_iters;
+            W[6] = dr_live;
+            W[7] = dr_taken;
         }
     }
     if (kCount) {

@@ -892,6 +892,8 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.ball_batch = env_int("RTNW_BALL_BATCH", RT_BALL_BATCH, 1, 64);
     a.ball_claim = env_int("RTNW_BALL_CLAIM", RT_BALL_CLAIM, 1, 64);
     a.ball_park = env_int("RTNW_BALL_PARK", 1, 0, 1);
+    a.ball_drain = env_int("RTNW_BALL_DRAIN", 1, 0, 1);
+    a.dry_batch = env_int("RTNW_DRY_BATCH", 64, 1, 64);
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = scene_features(s);
@@ -930,7 +932,7 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
         unsigned long long *&p;
         ~FreeOnExit() { if (p) (void)hipFree(p); }
     } wave_log_guard{wave_log};
-    const size_t wave_log_n = (size_t)s->grid[2] * ((s->lds_nodes ? RT_LDS_BLOCK : RT_BLOCK) / 64) * 5;
+    const size_t wave_log_n = (size_t)s->grid[2] * ((s->lds_nodes ? RT_LDS_BLOCK : RT_BLOCK) / 64) * RT_WAVE_LOG_WORDS;
     if (wave_log_path) {
         HIP_TRY(hipMalloc(&wave_log, wave_log_n * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(wave_log, 0, wave_log_n * sizeof(unsigned long long), stream));

@@ -43,7 +43,7 @@ def main():
     raw = np.fromfile(path, dtype=np.uint64)
     if args.out:
         raw.tofile(os.path.splitext(args.out)[0] + ".bin")
-    w = raw.reshape(-1, 5)
+    w = raw.reshape(-1, 8)   # RT_WAVE_LOG_WORDS (rt_kernel.h)
     print("records", len(w), "zero starts", int((w[:, 0] == 0).sum()), "first", w[:3].tolist(), file=sys.stderr)
     t0 = w[:, 0].min()
     start, dry, end = [(w[:, k] - t0).astype(np.float64) * 0.01 for k in range(3)]   # us
@@ -52,6 +52,9 @@ def main():
     slot, simd, cu = hw & 0xF, (hw >> 4) & 0x3, (hw >> 8) & 0xF
     se = (hw >> 13) & 0x7
     items = w[:, 4].astype(np.float64)
+    # after the wave's dry point: iterations, live lanes summed over them, pooled paths taken
+    d_it, d_live, d_taken = (w[:, k].astype(np.float64) for k in (5, 6, 7))
+    ball = (np.arange(len(w)) % 16) >= 16 - 3   # the ball waves (RT_BALL_WAVES, the LDS mode's 16-wave groups)
     q = lambda a: {f"p{k}": float(np.percentile(a, k)) for k in (0, 10, 50, 90, 99, 100)}   # noqa: E731
     res = {"config": args.config, "spp": spp, "waves": int(len(w)), "kernel_ms": st["kernel_ms"],
            "end_us": q(end), "dry_us": q(dry), "end_minus_dry_us": q(end - dry), "items": q(items),
@@ -64,8 +67,18 @@ def main():
            "items_by_se": {int(x): float(items[se == x].mean()) for x in np.unique(se)},
            "items_by_cu_p": q(np.bincount(cu + 16 * (se + 8 * xcc), weights=items)[np.bincount(cu + 16 * (se + 8 * xcc)) > 0]),
            "corr_items_end": float(np.corrcoef(items, end)[0, 1]),
+           # the drain: how long an iteration takes once the claims are exhausted, at how many lanes
+           "drain_iters": q(d_it), "drain_us_per_iter": q((end - dry) / np.maximum(d_it, 1)),
+           "drain_live_per_iter": q(d_live / np.maximum(d_it, 1)), "drain_taken": q(d_taken),
+           "drain_us_per_iter_ball": float(((end - dry) / np.maximum(d_it, 1))[ball].mean()),
+           "drain_us_per_iter_norm": float(((end - dry) / np.maximum(d_it, 1))[~ball].mean()),
+           "end_ball_vs_norm": [float(end[ball].mean()), float(end[~ball].mean())],
+           # wave-time idle between a wave's end and the launch's last end, over waves x (last end - first dry)
+           "drain_idle_frac": float((end.max() - end).sum() / (len(end) * (end.max() - dry.min()))),
            "last_10_waves": [{"end": float(end[i]), "dry": float(dry[i]), "items": float(items[i]), "xcc": int(xcc[i]),
-                              "se": int(se[i]), "cu": int(cu[i]), "simd": int(simd[i]), "slot": int(slot[i])}
+                              "se": int(se[i]), "cu": int(cu[i]), "simd": int(simd[i]), "slot": int(slot[i]),
+                              "ball": bool(ball[i]), "drain_iters": int(d_it[i]), "drain_live": float(d_live[i] / max(d_it[i], 1)),
+                              "drain_taken": int(d_taken[i])}
                              for i in np.argsort(end)[-10:]]}
     text = json.dumps(res, indent=1)
     print(text)
