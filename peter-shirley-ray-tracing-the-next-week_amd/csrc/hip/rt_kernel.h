@@ -25,7 +25,7 @@
 #define RT_FEAT_MEDIA 16    // constant_medium (without it: no media stage, no medium-stream key per sample)
 #define RT_FEAT_ALL 31
 
-#define RT_WAVE_LOG_WORDS 8
+#define RT_WAVE_LOG_WORDS 12
 
 struct RtKernelArgs {
     // scene (HBM, 16-B records; see rt_layout.h)
@@ -59,7 +59,6 @@ struct RtKernelArgs {
     int ball_claim;           //     ... and the busy lanes below which they claim new samples ...
     int ball_park;            //     ... and whether their segments the cell does not decide move to normal waves
     int ball_drain;           //     ... and whether, with the claims exhausted, normal waves leave the ball's pool to them
-    int dry_batch;            // a dry wave's ready batch (RT_DRY_LANES live lanes or fewer; 64: the normal one)
     int lds_nodes;          // 1: BVH2 nodes copied to LDS (RT_LDS_BLOCK workgroups, one per CU)
     int stack_depth;        // traversal stack entries per lane of the LDS variant (BVH depth + 1)
     // camera (camera.h members)
@@ -86,7 +85,8 @@ struct RtKernelArgs {
     uint32_t *counter;        // work-claim counter (zeroed per launch)
     unsigned long long *stats;  // RT_CNT_N counters (count variant)
     // profile variant, RTNW_WAVE_LOG: RT_WAVE_LOG_WORDS per wave (start, dry, end, hw id, items,
-    // iterations after dry, live lanes summed over them, paths taken from the pools after dry)
+    // iterations after dry, live lanes summed over them, paths taken from the pools after dry,
+    // the stage cycles after dry: claim, traverse, media, shade)
     unsigned long long *wave_log;
 };
 

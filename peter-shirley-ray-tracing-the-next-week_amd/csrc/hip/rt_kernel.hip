@@ -252,10 +252,12 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
     uint64_t rt_exhaust = 0;
     uint32_t rt_items = 0;   // work items this wave claimed (kProf)
     uint64_t dr_iters = 0, dr_live = 0, dr_taken = 0;   // (kProf) after the dry point: iterations, live lanes, pooled paths taken
+    uint64_t dr_prof[4] = {0, 0, 0, 0};                 // (kProf) ... and the stage cycles (claim, traverse, media, shade)
     auto mark = [&](int k) {
         if (kProf) {
             const uint64_t now = __builtin_amdgcn_s_memtime();
             prof[k] += now - stamp;
+            if (exhausted) dr_prof[k < 4 ? k : 3] += now - stamp;
             stamp = now;
         }
     };
@@ -675,11 +677,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             const int batch = ballrole ? A.ball_batch : RT_READY_BATCH;
             for (;;) {
                 if (wballot(phase == PH_TRAV) == 0ull) break;
-                // (A.dry_batch) a dry wave holds fewer lanes than the batch, and its iteration waits for
-                // the slowest lane's search (17 us in the drain against ~11 in the steady state,
-                // profiles/r06/wave_drain*.json): it shades once A.dry_batch lanes are ready
-                const uint32_t nready = (uint32_t)__popcll(wballot(phase == PH_READY));
-                if (nready >= (uint32_t)batch || (dry && nready >= (uint32_t)A.dry_batch)) break;
+                if (__popcll(wballot(phase == PH_READY)) >= batch) break;
                 if (kCount && ballrole && lane == 0) cnt.ball[RT_BALL_ROUNDS]++;
                 if (phase == PH_TRAV) {
                     // the slab test needs no exact division: boxes are padded (bvh.cpp)
@@ -869,6 +867,7 @@ __global__ __launch_bounds__(kMode == 1 ? RT_LDS_BLOCK : RT_BLOCK, RT_WAVES_PER_
             W[5] = dr_iters;
             W[6] = dr_live;
             W[7] = dr_taken;
+            for (int k = 0; k < 4; ++k) W[8 + k] = dr_prof[k];
         }
     }
     if (kCount) {

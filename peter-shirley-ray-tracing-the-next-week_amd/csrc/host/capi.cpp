@@ -893,7 +893,6 @@ int rt_render_tiles(rt_scene *s, const rt_camera_desc *cam, const rt_render_para
     a.ball_claim = env_int("RTNW_BALL_CLAIM", RT_BALL_CLAIM, 1, 64);
     a.ball_park = env_int("RTNW_BALL_PARK", 1, 0, 1);
     a.ball_drain = env_int("RTNW_BALL_DRAIN", 1, 0, 1);
-    a.dry_batch = env_int("RTNW_DRY_BATCH", 64, 1, 64);
     a.nprims = (uint32_t)s->nprims;
     a.stack_depth = s->stack_depth;
     a.features = scene_features(s);

@@ -575,7 +575,7 @@ def test_ball_waves_leave_the_image_bitwise_unchanged(monkeypatch):
     # ball waves that traverse their undecided segments themselves, that claim new samples
     # only when wholly idle, on a job of one 8 x 8 block (the claims exhausted at once)
     for env in ({"RTNW_BALL_PARK": "0"}, {"RTNW_BALL_CLAIM": "1"}, {"RTNW_BALL_WAVES": "16", "RTNW_BALL_CLAIM": "1"},
-                {"RTNW_BALL_DRAIN": "0"}, {"RTNW_DRY_BATCH": "1"}):
+                {"RTNW_BALL_DRAIN": "0"}):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         img = sc.render_tile(cam, rtnw.RenderParams(nx, ny, ns, seed=33), 0, 0, nx, ny)

@@ -43,7 +43,7 @@ def main():
     raw = np.fromfile(path, dtype=np.uint64)
     if args.out:
         raw.tofile(os.path.splitext(args.out)[0] + ".bin")
-    w = raw.reshape(-1, 8)   # RT_WAVE_LOG_WORDS (rt_kernel.h)
+    w = raw.reshape(-1, 12)   # RT_WAVE_LOG_WORDS (rt_kernel.h)
     print("records", len(w), "zero starts", int((w[:, 0] == 0).sum()), "first", w[:3].tolist(), file=sys.stderr)
     t0 = w[:, 0].min()
     start, dry, end = [(w[:, k] - t0).astype(np.float64) * 0.01 for k in range(3)]   # us
@@ -55,6 +55,8 @@ def main():
     # after the wave's dry point: iterations, live lanes summed over them, pooled paths taken
     d_it, d_live, d_taken = (w[:, k].astype(np.float64) for k in (5, 6, 7))
     ball = (np.arange(len(w)) % 16) >= 16 - 3   # the ball waves (RT_BALL_WAVES, the LDS mode's 16-wave groups)
+    dcyc = w[:, 8:12].astype(np.float64)   # stage cycles after the dry point
+    dshare = lambda m: [float(x) for x in (dcyc[m].sum(0) / max(dcyc[m].sum(), 1))]   # noqa: E731
     q = lambda a: {f"p{k}": float(np.percentile(a, k)) for k in (0, 10, 50, 90, 99, 100)}   # noqa: E731
     res = {"config": args.config, "spp": spp, "waves": int(len(w)), "kernel_ms": st["kernel_ms"],
            "end_us": q(end), "dry_us": q(dry), "end_minus_dry_us": q(end - dry), "items": q(items),
@@ -73,6 +75,10 @@ def main():
            "drain_us_per_iter_ball": float(((end - dry) / np.maximum(d_it, 1))[ball].mean()),
            "drain_us_per_iter_norm": float(((end - dry) / np.maximum(d_it, 1))[~ball].mean()),
            "end_ball_vs_norm": [float(end[ball].mean()), float(end[~ball].mean())],
+           # where a drain iteration's cycles go (claim, traverse, media, shade), and its cycles
+           "drain_stage_share_norm": dshare(~ball), "drain_stage_share_ball": dshare(ball),
+           "drain_cycles_per_iter_norm": float(dcyc[~ball].sum() / max(d_it[~ball].sum(), 1)),
+           "drain_cycles_per_iter_ball": float(dcyc[ball].sum() / max(d_it[ball].sum(), 1)),
            # wave-time idle between a wave's end and the launch's last end, over waves x (last end - first dry)
            "drain_idle_frac": float((end.max() - end).sum() / (len(end) * (end.max() - dry.min()))),
            "last_10_waves": [{"end": float(end[i]), "dry": float(dry[i]), "items": float(items[i]), "xcc": int(xcc[i]),
