@@ -49,8 +49,12 @@ def main():
         src = os.path.join(out, "final_" + cfg)
         dst = prof if cfg == "c4" else os.path.join(prof, cfg)
         os.makedirs(dst, exist_ok=True)
-        subprocess.run([sys.executable, os.path.join(HERE, "pmc_traffic.py"), src, dst, str(samples_of(cfg)), cfg],
-                       check=True, env=env, stdout=subprocess.DEVNULL)
+        r = subprocess.run([sys.executable, os.path.join(HERE, "pmc_traffic.py"), src, dst, str(samples_of(cfg)), cfg],
+                           env=env, stdout=subprocess.DEVNULL)
+        if r.returncode == 3:   # counters of another build (pmc_traffic.py): left out
+            print("profile", cfg, "skipped: another build's counters")
+            continue
+        r.check_returncode()
         pd = os.path.join(prof, "pmc", cfg)
         for k in ("fetch", "write", "l2", "sq", "lds"):
             cp(os.path.join(src, f"pmc_{k}", "run_counter_collection.csv"), os.path.join(pd, f"pmc_{k}.csv"))

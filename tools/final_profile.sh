@@ -15,7 +15,9 @@ export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 CFG=${1:-c4}   # the bench config profiled (c4 = the metric's; c2, c3, c5 for their own bench lines;
                # c5_nN: one rank's share of c5 split over N GPUs, bench.py --share-of N)
 O=gpurun_out/final_$CFG
-mkdir -p $O/classes
+mkdir -p $O/classes gpurun_out/lanes_$CFG
+# the device code these passes run: the host-side summaries refuse counters of another build
+python3 -c "import bench; print(bench.kernel_sha16())" | tee $O/kernel_sha16.txt > gpurun_out/lanes_$CFG/kernel_sha16.txt
 case $CFG in
   c5_n*) B="python3 bench.py --share-of ${CFG#c5_n} --steps 1 --warmup 0 --no-cpu-baseline" ;;
   *)     B="python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline" ;;

@@ -54,6 +54,10 @@ def main():
         csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         if not csvs:
             continue
+        rec = os.path.join(d, "kernel_sha16.txt")   # tools/final_profile.sh: the build the passes ran
+        if os.path.exists(rec) and open(rec).read().strip() != res.get("kernel_sha16"):
+            print(f"{d}: counters of kernel {open(rec).read().strip()}, not this library's: skipped", file=sys.stderr)
+            continue
         v = first_dispatch(csvs[0])
         if "SQ_THREAD_CYCLES_VALU" in v and v.get("SQ_ACTIVE_INST_VALU"):
             v["lane_utilisation"] = v["SQ_THREAD_CYCLES_VALU"] / (64 * v["SQ_ACTIVE_INST_VALU"])

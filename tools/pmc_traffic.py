@@ -63,8 +63,15 @@ def main():
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
+    ksha = bench.kernel_sha16(lib)
+    # counters taken on another build (a stale gpurun_out/ directory) are not this library's
+    rec = os.path.join(out, "kernel_sha16.txt")
+    if os.path.exists(rec) and open(rec).read().strip() != ksha:
+        print(f"{out}: counters of kernel {open(rec).read().strip()}, the library here is {ksha}: not summarised",
+              file=sys.stderr)
+        sys.exit(3)
     res = {"config": config, "workload": f"{config} (bench.py --config {config})", "samples_per_launch": samples,
-           "lib_sha16": sha, "kernel_sha16": bench.kernel_sha16(lib)}
+           "lib_sha16": sha, "kernel_sha16": ksha}
     if fetch and write:
         fb = fetch["FETCH_SIZE"] * 1024.0
         wb = write["WRITE_SIZE"] * 1024.0
