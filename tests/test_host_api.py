@@ -328,3 +328,13 @@ def test_math_probe_rejects_bad_arguments():
     assert L.rt_math_probe(4, x.ctypes.data, None, out.ctypes.data, 4) == RT_ERR_INVALID   # atan2f needs b
     assert L.rt_math_probe(0, None, None, out.ctypes.data, 4) == RT_ERR_INVALID
     assert L.rt_math_probe(0, None, None, None, 0) == rtnw.RT_OK   # nothing to do
+
+
+def test_wave_log_record_size_matches_the_reader():
+    """tools/wave_log.py reads the profile variant's per-wave records (RTNW_WAVE_LOG) in
+    RT_WAVE_LOG_WORDS words each (rt_kernel.h; capi.cpp sizes the buffer by it)."""
+    import re
+    hdr = open(os.path.join(ROOT, "peter-shirley-ray-tracing-the-next-week_amd", "csrc", "hip", "rt_kernel.h")).read()
+    words = int(re.search(r"#define RT_WAVE_LOG_WORDS (\d+)", hdr).group(1))
+    tool = open(os.path.join(ROOT, "tools", "wave_log.py")).read()
+    assert f"raw.reshape(-1, {words})" in tool
