@@ -697,10 +697,11 @@ int rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
 
 // Waves per LDS workgroup that gather the medium cell's paths (rt_kernel.hip stage 6);
 // env RTNW_BALL_WAVES (0: none) for A/B runs.  Their ready batch (RTNW_BALL_BATCH) and the
-// busy lanes below which they claim new samples (RTNW_BALL_CLAIM).
+// busy lanes below which they claim new samples (RTNW_BALL_CLAIM): 56 and 48 against 48 and
+// 64, c4 48.87 -> 48.50 ms, the share of 8 25.20 -> 25.05 ms (profiles/r06/knobs3_ab.log).
 #define RT_BALL_WAVES 3
-#define RT_BALL_BATCH 48
-#define RT_BALL_CLAIM 64
+#define RT_BALL_BATCH 56
+#define RT_BALL_CLAIM 48
 static int env_int(const char *name, int dflt, int lo, int hi) {
     if (const char *e = std::getenv(name)) return std::max(lo, std::min(hi, std::atoi(e)));
     return dflt;
